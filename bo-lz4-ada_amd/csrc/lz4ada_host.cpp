@@ -1,0 +1,1198 @@
+// lz4ada_host.cpp -- host side of the MI355X LZ4Ada decompressor: the frame
+// engine (header parser and Update state machine of lib/lz4ada.adb, L2 of
+// SURVEY §1), the bulk frame indexer, and the C-ABI of include/lz4ada_hip.h.
+//
+// The host only parses framing.  Every block byte is produced on the GPU:
+// the streaming Update path runs k_serial_block (reference-exact, one
+// block per call) on a device mirror of the caller's Buffer; the bulk path
+// runs k_decode_blocks (one wavefront per block) over a whole frame.  There
+// is no CPU decoder here: without a GPU, decoding calls fail with
+// LZ4ADA_DEVICE_ERROR.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "lz4ada_hip.h"
+#include "lz4ada_internal.h"
+
+namespace lz4ada {
+
+// ------------------------------------------------------------------ errors
+
+struct Error {
+	int code;
+	std::string msg;
+};
+
+[[noreturn]] static void raise(int code, std::string msg) { throw Error{ code, std::move(msg) }; }
+
+// Ada 'Image: leading blank for non-negative numbers.
+static std::string img(int64_t v)
+{
+	return v >= 0 ? " " + std::to_string(v) : std::to_string(v);
+}
+static std::string img_u(uint64_t v) { return " " + std::to_string(v); }
+static std::string hex8(uint32_t v)
+{
+	char b[8];
+	snprintf(b, sizeof b, "%02x", v & 0xffu);
+	return b;
+}
+static std::string hex32(uint32_t v)
+{
+	char b[16];
+	snprintf(b, sizeof b, "%08x", v);
+	return b;
+}
+
+static const char* const RES_IMAGE[] = { "SZ_64_KIB", "SZ_256_KIB", "SZ_1_MIB",    "SZ_4_MIB",
+	                                 "SZ_8_MIB",  "USE_FIRST",  "SINGLE_FRAME" };
+
+static thread_local std::string g_thread_error;
+
+static uint32_t load32(const uint8_t* p)
+{
+	return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) |
+	       (uint32_t(p[3]) << 24);
+}
+static uint64_t load64(const uint8_t* p) { return uint64_t(load32(p)) | (uint64_t(load32(p + 4)) << 32); }
+
+// XXH32 of the 2..14-byte frame descriptor for the header checksum byte
+// (lz4ada.adb:351-361).  Framing, not block data: it runs on the host.
+static uint32_t descriptor_xxh32(const uint8_t* p, size_t n)
+{
+	auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+	uint32_t h = uint32_t(n) + P5;  // n < 16: no stripes
+	size_t d = 0;
+	for (; d + 4 <= n; d += 4)
+		h = rotl(h + load32(p + d) * P3, 17) * P4;
+	for (; d < n; ++d)
+		h = rotl(h + uint32_t(p[d]) * P5, 11) * P1;
+	h = (h ^ (h >> 15)) * P2;
+	h = (h ^ (h >> 13)) * P3;
+	return h ^ (h >> 16);
+}
+
+// ------------------------------------------------------------------ device
+
+#define HIP_OK(expr)                                                                          \
+	do {                                                                                  \
+		hipError_t _e = (expr);                                                       \
+		if (_e != hipSuccess)                                                         \
+			raise(LZ4ADA_DEVICE_ERROR,                                            \
+			      std::string("HIP error: ") + hipGetErrorString(_e) + " at " #expr); \
+	} while (0)
+
+static void device_check_or_raise()
+{
+	int n = 0;
+	hipError_t e = hipGetDeviceCount(&n);
+	if (e != hipSuccess || n <= 0)
+		raise(LZ4ADA_DEVICE_ERROR,
+		      "no usable HIP device: the LZ4Ada MI355X decoder has no CPU fallback");
+}
+
+template <class T>
+struct DevBuf {
+	T* p = nullptr;
+	size_t n = 0;  // elements
+	DevBuf() = default;
+	DevBuf(const DevBuf&) = delete;
+	DevBuf& operator=(const DevBuf&) = delete;
+	~DevBuf() { release(); }
+	void release()
+	{
+		if (p)
+			(void)hipFree(p);
+		p = nullptr;
+		n = 0;
+	}
+	void reserve(size_t count)
+	{
+		if (count <= n && p)
+			return;
+		release();
+		HIP_OK(hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T) + 64));
+		n = count;
+	}
+};
+
+// ------------------------------------------------------------------ meta
+
+enum Fmt { F_TBD, F_LEGACY, F_MODERN, F_BLOCK, F_SKIPPABLE };               // lz4ada.ads:355
+enum Hps { NEED_MAGIC, NEED_MODERN, NEED_FLAGS, NEED_SKIP_LEN, HDR_DONE };  // lz4ada.ads:356
+
+constexpr uint32_t MAGIC_MODERN = 0x184d2204u;  // lz4ada.ads:348-353
+constexpr uint32_t MAGIC_LEGACY = 0x184c2102u;
+constexpr uint32_t MAGIC_SKIP_LO = 0x184d2a50u, MAGIC_SKIP_HI = 0x184d2a5fu;
+
+struct Meta {  // Decompressor_Meta, lz4ada.ads:359-370
+	int is_format = F_TBD;
+	int header_parsing = NEED_MAGIC;
+	int memory_reservation = LZ4ADA_FOR_ALL;
+	int content_checksum_length = 0;
+	int block_checksum_length = 0;
+	int status_eof = LZ4ADA_EOF_NO;
+	int64_t input_buffer_filled = 0;
+	bool is_compressed = false;
+	bool has_content_size = false;
+	uint64_t size_remaining = 4;
+	// frame descriptor facts the reference does not keep (bulk path)
+	uint8_t flg = 0, bd = 0;
+};
+
+static bool concrete(int r) { return r >= LZ4ADA_SZ_64_KIB && r <= LZ4ADA_SZ_8_MIB; }
+
+static int64_t block_size_of(int r)  // Get_Block_Size, lz4ada.adb:65-77
+{
+	static const int64_t lut[] = { 64 << 10, 256 << 10, 1 << 20, 4 << 20, 8 << 20 };
+	return lut[r];
+}
+
+static void check_reservation(int requested, int& effective)  // lz4ada.adb:241-260
+{
+	if (concrete(requested)) {
+		if (effective > requested)
+			raise(LZ4ADA_TOO_LITTLE_MEMORY,
+			      std::string("LZ4 header requres reservation ") + RES_IMAGE[effective] +
+			              ", but API call requested that only " + RES_IMAGE[requested] +
+			              " be used. This frame cannot be processed under the given "
+			              "constraints.");
+		effective = requested;
+	}
+}
+
+static void legacy_end_of_header(Meta& m)  // lz4ada.adb:225-239
+{
+	int eff = LZ4ADA_FOR_LEGACY;
+	m.input_buffer_filled = 0;
+	m.is_format = F_LEGACY;
+	m.header_parsing = HDR_DONE;
+	m.size_remaining = 0;
+	m.status_eof = LZ4ADA_EOF_MAYBE;
+	m.block_checksum_length = 0;
+	m.content_checksum_length = 0;
+	m.has_content_size = false;
+	m.is_compressed = true;
+	check_reservation(m.memory_reservation, eff);
+	m.memory_reservation = eff;
+}
+
+static void header_magic(Meta& m, uint32_t magic)  // lz4ada.adb:199-223
+{
+	if (magic == MAGIC_MODERN) {
+		m.is_format = F_MODERN;
+		m.header_parsing = NEED_FLAGS;
+		m.size_remaining = 2;
+	} else if (magic == MAGIC_LEGACY) {
+		legacy_end_of_header(m);
+	} else if (magic >= MAGIC_SKIP_LO && magic <= MAGIC_SKIP_HI) {
+		m.is_format = F_SKIPPABLE;
+		m.header_parsing = NEED_SKIP_LEN;
+		m.size_remaining = 4;
+		m.block_checksum_length = 0;
+		m.content_checksum_length = 0;
+	} else {
+		raise(LZ4ADA_NOT_SUPPORTED, "Invalid or unsupported magic: 0x" + hex32(magic));
+	}
+}
+
+static void header_flags(Meta& m, const uint8_t* hb)  // lz4ada.adb:262-328
+{
+	const uint8_t flg = hb[4], bd = hb[5];
+	const unsigned version = (flg & 0xc0u) >> 6, bmax = (bd & 0x70u) >> 4;
+	if (version != 1)
+		raise(LZ4ADA_NOT_SUPPORTED, "Only LZ4 frame format version 01 supported. Detected 0x" +
+		                                    hex8(version) + " instead.");
+	if ((flg & 2u) || (bd & 0x8fu))
+		raise(LZ4ADA_NOT_SUPPORTED,
+		      "Found reserved bits /= 0. Data might be too new to be processed by this "
+		      "implementation!");
+	m.status_eof = LZ4ADA_EOF_NO;
+	int required;
+	switch (bmax) {
+	case 4: required = LZ4ADA_SZ_64_KIB; break;
+	case 5: required = LZ4ADA_SZ_256_KIB; break;
+	case 6: required = LZ4ADA_SZ_1_MIB; break;
+	case 7: required = LZ4ADA_SZ_4_MIB; break;
+	default: raise(LZ4ADA_NOT_SUPPORTED, "Unknown maximum block size flag: 0x" + hex8(bmax));
+	}
+	m.flg = flg;
+	m.bd = bd;
+	m.block_checksum_length = (flg & 16u) ? 4 : 0;
+	m.content_checksum_length = (flg & 4u) ? 4 : 0;
+	m.has_content_size = (flg & 8u) != 0;
+	m.header_parsing = NEED_MODERN;
+	m.size_remaining = 1 + (m.has_content_size ? 8 : 0) + ((flg & 1u) ? 4 : 0);
+	check_reservation(m.memory_reservation, required);
+	if (m.memory_reservation != LZ4ADA_SINGLE_FRAME)
+		m.memory_reservation = required;
+}
+
+static void header_modern_end(Meta& m, const uint8_t* hb)  // lz4ada.adb:330-361
+{
+	const uint8_t hc = hb[m.input_buffer_filled - 1];
+	if (m.has_content_size)
+		m.size_remaining = load64(hb + 6);
+	const uint8_t computed =
+	        uint8_t((descriptor_xxh32(hb + 4, size_t(m.input_buffer_filled - 1 - 4)) >> 8) & 0xffu);
+	if (hc != computed)
+		raise(LZ4ADA_CHECKSUM_ERROR, "Computed Header Checksum 0x" + hex8(computed) +
+		                                     " does not match expected Header Checksum 0x" +
+		                                     hex8(hc));
+	m.header_parsing = HDR_DONE;
+	m.input_buffer_filled = 0;
+}
+
+// Process_Header_Bytes (lz4ada.adb:155-191)
+static int64_t header_bytes(Meta& m, uint8_t* hb, const uint8_t* in, int64_t len)
+{
+	const int64_t copy = std::min<int64_t>(len, int64_t(m.size_remaining));
+	if (!(copy > 0))
+		raise(LZ4ADA_ASSERTION_ERROR, "lz4ada.adb:161");
+	memcpy(hb + m.input_buffer_filled, in, size_t(copy));
+	m.input_buffer_filled += copy;
+	m.size_remaining -= uint64_t(copy);
+	if (m.size_remaining == 0) {
+		switch (m.header_parsing) {
+		case NEED_MAGIC: header_magic(m, load32(hb)); break;
+		case NEED_FLAGS: header_flags(m, hb); break;
+		case NEED_MODERN: header_modern_end(m, hb); break;
+		case NEED_SKIP_LEN:
+			m.memory_reservation = LZ4ADA_SZ_64_KIB;  // quirk Q3
+			m.header_parsing = HDR_DONE;
+			m.size_remaining = load32(hb + 4);
+			m.status_eof = m.size_remaining == 0 ? LZ4ADA_EOF_YES : LZ4ADA_EOF_NO;
+			m.input_buffer_filled = 0;
+			break;
+		default:
+			raise(LZ4ADA_CONSTRAINT_ERROR,
+			      "Header_Complete case must not be reached while processing header bytes. "
+			      "Library bug detected.");
+		}
+	}
+	return copy;
+}
+
+static bool is_any_magic(uint32_t v)
+{
+	return v == MAGIC_MODERN || v == MAGIC_LEGACY || (v >= MAGIC_SKIP_LO && v <= MAGIC_SKIP_HI);
+}
+
+// Device status of a decode kernel -> the reference's exception.
+[[noreturn]] static void raise_device_status(const SerialState& s)
+{
+	switch (s.code) {
+	case DS_OFFSET0: raise(LZ4ADA_DATA_CORRUPTION, "Corrupted Block: Offset = 0 detected.");
+	case DS_ML_AFTER_LIT:
+		raise(LZ4ADA_DATA_CORRUPTION,
+		      "Match_Length=" + img(s.aux) +
+		              " suggests compressed data but this sequence already ends after the "
+		              "literals. This might also happen with an untypical encoder?");
+	case DS_LIT_OVERRUN:
+		raise(LZ4ADA_DATA_CORRUPTION, "Corrupted Block: literal run exceeds the end of the block.");
+	case DS_TRUNCATED:
+		raise(LZ4ADA_DATA_CORRUPTION,
+		      "Corrupted Block: sequence truncated at the end of the block.");
+	case DS_OUT_OVERFLOW:
+		raise(LZ4ADA_DATA_CORRUPTION,
+		      "Corrupted Block: decompressed data exceeds the output buffer.");
+	case DS_BACKREF:
+		raise(LZ4ADA_DATA_CORRUPTION, "Backreference location out of range. Read from offset " +
+		                                      img(s.detail) +
+		                                      " not possible (earliest available index is 0).");
+	case DS_CONTENT_SIZE:
+		raise(LZ4ADA_DATA_CORRUPTION,
+		      "Produced content size exceeds declared content size. The supplied data is "
+		      "inconsistent.");
+	default: raise(LZ4ADA_CONSTRAINT_ERROR, "unexpected device status " + std::to_string(s.code));
+	}
+}
+
+}  // namespace lz4ada
+
+using namespace lz4ada;
+
+// ----------------------------------------------------------- Decompressor
+
+struct lz4ada_decompressor {
+	Meta m;
+	bool is_at_end_mark = false;
+	std::vector<uint8_t> input_buffer;  // Input_Buffer(0 .. In_Last)
+	int64_t output_pos = 0;
+	int64_t output_pos_history = 0;
+	int64_t input_length = -1;
+	std::string err;
+
+	// device side (lazily created at the first block)
+	bool dev_ready = false;
+	int device = -1;
+	hipStream_t stream = nullptr;
+	DevBuf<uint8_t> d_buf;  // mirror of the caller's Buffer (history lives here)
+	int64_t d_buf_len = 0;
+	DevBuf<uint8_t> d_blk;
+	DevBuf<lz4ada_xxh32_state> d_hash;  // Hash_All_Data
+	DevBuf<lz4ada_xxh32_state> d_tmp_hash;
+	DevBuf<SerialState> d_serial;
+
+	~lz4ada_decompressor()
+	{
+		if (stream) {
+			(void)hipStreamSynchronize(stream);
+			(void)hipStreamDestroy(stream);
+		}
+	}
+
+	void ensure_device()
+	{
+		if (dev_ready)
+			return;
+		device_check_or_raise();
+		HIP_OK(hipGetDevice(&device));
+		HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+		d_hash.reserve(1);
+		d_tmp_hash.reserve(1);
+		d_serial.reserve(1);
+		dev_ready = true;
+		reset_content_hash();
+	}
+
+	void reset_content_hash()  // XXHash32.Reset(0) on the device state
+	{
+		if (!dev_ready)
+			return;
+		lz4ada_xxh32_state h;
+		lz4ada_xxh32_reset(&h, 0);
+		HIP_OK(hipMemcpyAsync(d_hash.p, &h, sizeof h, hipMemcpyHostToDevice, stream));
+	}
+
+	// ---------------------------------------------------- Update pieces
+	void reset_outer()  // lz4ada.adb:451-461
+	{
+		is_at_end_mark = false;
+		input_length = -1;
+		output_pos = 0;
+		output_pos_history = 0;
+		reset_content_hash();
+	}
+
+	int64_t reset_for_next_frame(const uint8_t* in, int64_t len)  // :435-449
+	{
+		if (m.memory_reservation == LZ4ADA_SINGLE_FRAME)
+			raise(LZ4ADA_DATA_CORRUPTION,
+			      "Requested Single_Frame operation but data was provided after End of Frame "
+			      "was detected");
+		m.status_eof = LZ4ADA_EOF_NO;
+		m.header_parsing = NEED_MAGIC;
+		m.size_remaining = 4;
+		reset_outer();
+		return header_bytes(m, input_buffer.data(), in, len);
+	}
+
+	int64_t skip(const uint8_t* in, int64_t len)  // :420-433
+	{
+		const uint64_t remain = m.size_remaining;
+		const uint64_t cons = std::min<uint64_t>(uint64_t(len), remain);
+		if (m.status_eof == LZ4ADA_EOF_YES && cons == 0)
+			return reset_for_next_frame(in, len);
+		m.size_remaining = remain - cons;
+		m.status_eof = m.size_remaining == 0 ? LZ4ADA_EOF_YES : LZ4ADA_EOF_NO;
+		return int64_t(cons);
+	}
+
+	void frame_has_ended()  // :465-477
+	{
+		m.status_eof = LZ4ADA_EOF_YES;
+		m.input_buffer_filled = 0;
+		if (m.has_content_size && m.size_remaining != 0)
+			raise(LZ4ADA_DATA_CORRUPTION,
+			      "Frame has ended, but according to content size, there should be " +
+			              img_u(m.size_remaining) + " bytes left to output.");
+	}
+
+	uint32_t content_hash_final()
+	{
+		ensure_device();
+		// refresh the cached Final() on the device (len = 0 update)
+		HIP_OK(launch_xxh32_update(d_hash.p, nullptr, 0, stream));
+		lz4ada_xxh32_state h;
+		HIP_OK(hipMemcpyAsync(&h, d_hash.p, sizeof h, hipMemcpyDeviceToHost, stream));
+		HIP_OK(hipStreamSynchronize(stream));
+		return h.hash;
+	}
+
+	void check_end_mark(const uint8_t* in, int64_t len, int64_t& consumed)  // :463-523
+	{
+		const int64_t provided = len - consumed;
+		const int64_t required = m.content_checksum_length - m.input_buffer_filled;
+		if (m.content_checksum_length == 0 || m.status_eof == LZ4ADA_EOF_YES || required <= 0) {
+			if (m.status_eof == LZ4ADA_EOF_YES) {
+				if (consumed != 0)
+					raise(LZ4ADA_ASSERTION_ERROR, "lz4ada.adb:486");
+				consumed = reset_for_next_frame(in, len);
+			} else {
+				frame_has_ended();
+			}
+		} else if (provided >= required) {
+			uint8_t tmp[8];
+			memcpy(tmp, input_buffer.data(), size_t(m.input_buffer_filled));
+			memcpy(tmp + m.input_buffer_filled, in + consumed, size_t(required));
+			const uint32_t declared = load32(tmp);
+			const uint32_t computed = content_hash_final();
+			consumed += required;
+			if (declared != computed)
+				raise(LZ4ADA_CHECKSUM_ERROR, "Computed content checksum 0x" + hex32(computed) +
+				                                     " does not match declared content checksum 0x" +
+				                                     hex32(declared) + ".");
+			frame_has_ended();
+		} else {
+			memcpy(input_buffer.data() + m.input_buffer_filled, in + consumed, size_t(provided));
+			m.input_buffer_filled += provided;
+			consumed += provided;
+		}
+	}
+
+	int64_t try_detect_input_length(const uint8_t* in, int64_t len)  // :525-585
+	{
+		const int64_t additional = BLOCK_SIZE_BYTES + m.block_checksum_length;
+		const int64_t n = std::min<int64_t>(BLOCK_SIZE_BYTES - m.input_buffer_filled, len);
+		memcpy(input_buffer.data() + m.input_buffer_filled, in, size_t(n));
+		m.input_buffer_filled += n;
+		if (m.input_buffer_filled == BLOCK_SIZE_BYTES) {
+			uint32_t word = load32(input_buffer.data());
+			if (m.is_format == F_MODERN && word == 0) {
+				is_at_end_mark = true;
+				m.input_buffer_filled = 0;
+			} else if (m.is_format == F_LEGACY && is_any_magic(word)) {
+				if (m.memory_reservation == LZ4ADA_SINGLE_FRAME)
+					raise(LZ4ADA_DATA_CORRUPTION,
+					      "Requested Single_Frame operation but data provided what looks "
+					      "like the beginning of another frame.");
+				reset_outer();
+				header_magic(m, word);
+			} else {
+				if (m.is_format == F_MODERN) {
+					m.is_compressed = (word & 0x80000000u) == 0;
+					word &= 0x7ffffffu;  // 27-bit mask, quirk Q2
+				}
+				input_length = int64_t(word);
+				if (input_length + additional > int64_t(input_buffer.size())) {
+					input_length = -1;
+					raise(LZ4ADA_DATA_CORRUPTION,
+					      "Declared maximum data length exceeded. Buffer has " +
+					              img(int64_t(input_buffer.size())) +
+					              " bytes, current block requires " + img_u(word) +
+					              " bytes + " + img(additional) + " bytes for metadata.");
+				}
+			}
+		}
+		return n;
+	}
+
+	// Decode_Full_Block_With_Trailer (lz4ada.adb:661-714) on the GPU.
+	void decode_full_block(const uint8_t* blk, int64_t blen, uint8_t* buf, int64_t buflen,
+	                       int64_t& first, int64_t& last)
+	{
+		ensure_device();
+		const int bcl = m.block_checksum_length;
+		const int64_t raw_len = blen - bcl;
+		if (buflen > d_buf_len) {  // grow the Buffer mirror, keeping history
+			DevBuf<uint8_t> nb;
+			nb.reserve(size_t(buflen));
+			HIP_OK(hipMemsetAsync(nb.p, 0, size_t(buflen), stream));
+			if (d_buf_len)
+				HIP_OK(hipMemcpyAsync(nb.p, d_buf.p, size_t(d_buf_len), hipMemcpyDeviceToDevice,
+				                      stream));
+			HIP_OK(hipStreamSynchronize(stream));
+			std::swap(nb.p, d_buf.p);
+			std::swap(nb.n, d_buf.n);
+			d_buf_len = buflen;
+		}
+		d_blk.reserve(size_t(std::max<int64_t>(blen, 1)));
+		if (blen > 0)
+			HIP_OK(hipMemcpyAsync(d_blk.p, blk, size_t(blen), hipMemcpyHostToDevice, stream));
+		if (bcl > 0) {  // Check_Checksum before decoding (:672-676, quirk Q8)
+			lz4ada_xxh32_state h;
+			lz4ada_xxh32_reset(&h, 0);
+			HIP_OK(hipMemcpyAsync(d_tmp_hash.p, &h, sizeof h, hipMemcpyHostToDevice, stream));
+			HIP_OK(launch_xxh32_update(d_tmp_hash.p, d_blk.p, uint64_t(raw_len), stream));
+			HIP_OK(hipMemcpyAsync(&h, d_tmp_hash.p, sizeof h, hipMemcpyDeviceToHost, stream));
+			HIP_OK(hipStreamSynchronize(stream));
+			const uint32_t expect = load32(blk + blen - bcl);
+			if (h.hash != expect)
+				raise(LZ4ADA_CHECKSUM_ERROR, "Declared checksum is 0x" + hex32(expect) +
+				                                     ", but computed one is 0x" + hex32(h.hash) +
+				                                     ".");
+		}
+		SerialState s{};
+		s.output_pos = output_pos;
+		s.output_pos_history = output_pos_history;
+		s.size_remaining = m.size_remaining;
+		s.has_content_size = m.has_content_size ? 1 : 0;
+		HIP_OK(hipMemcpyAsync(d_serial.p, &s, sizeof s, hipMemcpyHostToDevice, stream));
+		HIP_OK(launch_serial_block(d_buf.p, buflen, d_blk.p, raw_len,
+		                           m.is_compressed ? raw_len : blen, m.is_compressed ? 1 : 0,
+		                           d_serial.p, stream));
+		HIP_OK(hipMemcpyAsync(&s, d_serial.p, sizeof s, hipMemcpyDeviceToHost, stream));
+		HIP_OK(hipStreamSynchronize(stream));
+		// state changes before a raise persist, as with the Ada record
+		output_pos = s.output_pos;
+		output_pos_history = s.output_pos_history;
+		if (m.has_content_size)
+			m.size_remaining = s.size_remaining;
+		if (s.code != DS_OK)
+			raise_device_status(s);
+		first = s.first;
+		last = s.last;
+		const int64_t nout = last - first + 1;
+		if (nout > 0) {
+			if (m.content_checksum_length != 0)  // Update_Checksum (:709-714)
+				HIP_OK(launch_xxh32_update(d_hash.p, d_buf.p + first, uint64_t(nout), stream));
+			HIP_OK(hipMemcpyAsync(buf + first, d_buf.p + first, size_t(nout),
+			                      hipMemcpyDeviceToHost, stream));
+			HIP_OK(hipStreamSynchronize(stream));
+		}
+	}
+
+	void cache_and_process(const uint8_t* in, int64_t len, int64_t& consumed, uint8_t* buf,
+	                       int64_t buflen, int64_t& first, int64_t& last)  // :630-659
+	{
+		const int64_t avail = len - consumed;
+		const int64_t want = input_length + m.block_checksum_length - m.input_buffer_filled +
+		                     (m.is_format == F_BLOCK ? 0 : BLOCK_SIZE_BYTES);
+		const int64_t fill = m.input_buffer_filled;
+		const uint8_t* src = in + consumed;
+		if (want > avail) {
+			if (fill + avail > int64_t(input_buffer.size()))
+				raise(LZ4ADA_CONSTRAINT_ERROR, "lz4ada.adb:644 index check failed");
+			memcpy(input_buffer.data() + fill, src, size_t(avail));
+			m.input_buffer_filled += avail;
+			consumed += avail;
+		} else {
+			consumed += want;
+			m.input_buffer_filled = 0;
+			input_length = -1;
+			// Input_Buffer(4 .. Fill-1) & Input(...): drops 4 cached bytes for
+			// the raw-block format (quirk Q5), like the reference.
+			const int64_t head = std::max<int64_t>(fill - BLOCK_SIZE_BYTES, 0);
+			std::vector<uint8_t> blk(size_t(head + want));
+			if (head)
+				memcpy(blk.data(), input_buffer.data() + BLOCK_SIZE_BYTES, size_t(head));
+			memcpy(blk.data() + head, src, size_t(want));
+			decode_full_block(blk.data(), head + want, buf, buflen, first, last);
+		}
+	}
+
+	void update(const uint8_t* in, int64_t len, int64_t& consumed, uint8_t* buf, int64_t buflen,
+	            int64_t& first, int64_t& last)  // lz4ada.adb:383-418
+	{
+		consumed = 0;
+		first = 1;
+		last = 0;
+		if (m.header_parsing != HDR_DONE) {
+			consumed = header_bytes(m, input_buffer.data(), in, len);
+		} else if (m.is_format == F_SKIPPABLE) {
+			consumed = skip(in, len);
+		} else if (is_at_end_mark) {
+			check_end_mark(in, len, consumed);
+		} else if (input_length != -1) {
+			cache_and_process(in, len, consumed, buf, buflen, first, last);
+		} else {
+			consumed = try_detect_input_length(in, len);
+			if (is_at_end_mark) {
+				check_end_mark(in, len, consumed);
+			} else if (input_length != -1) {
+				const int64_t total = input_length + m.block_checksum_length;
+				if (len - consumed >= total) {  // :603-617, no copy
+					const uint8_t* blk = in + consumed;
+					consumed += total;
+					m.input_buffer_filled = 0;
+					input_length = -1;
+					decode_full_block(blk, total, buf, buflen, first, last);
+				} else {
+					cache_and_process(in, len, consumed, buf, buflen, first, last);
+				}
+			}
+		}
+	}
+
+	int is_end_of_frame() const  // :906-915
+	{
+		switch (m.is_format) {
+		case F_LEGACY: return is_at_end_mark ? LZ4ADA_EOF_MAYBE : m.status_eof;
+		case F_BLOCK: return input_length == -1 ? LZ4ADA_EOF_YES : LZ4ADA_EOF_NO;
+		default: return m.status_eof;
+		}
+	}
+};
+
+// ---------------------------------------------------------------- C-ABI
+
+template <class F>
+static int guarded(std::string* err, F&& f)
+{
+	try {
+		f();
+		if (err)
+			err->clear();
+		return LZ4ADA_OK;
+	} catch (const Error& e) {
+		if (err)
+			*err = e.msg;
+		g_thread_error = e.msg;
+		return e.code;
+	} catch (const std::bad_alloc&) {
+		if (err)
+			*err = "out of host memory";
+		g_thread_error = "out of host memory";
+		return LZ4ADA_CONSTRAINT_ERROR;
+	}
+}
+
+static lz4ada_decompressor* new_ctx(int64_t in_last)
+{
+	auto* c = new lz4ada_decompressor();
+	c->input_buffer.assign(size_t(std::max<int64_t>(in_last + 1, 0)), 0);
+	return c;
+}
+
+extern "C" {
+
+int lz4ada_abi_version(void) { return LZ4ADA_HIP_ABI_VERSION; }
+
+const char* lz4ada_error_name(int status)
+{
+	static const char* const names[] = { "",
+		                             "LZ4ADA.CHECKSUM_ERROR",
+		                             "LZ4ADA.DATA_CORRUPTION",
+		                             "LZ4ADA.NOT_SUPPORTED",
+		                             "LZ4ADA.TOO_FEW_HEADER_BYTES",
+		                             "LZ4ADA.TOO_LITTLE_MEMORY",
+		                             "ADA.ASSERTIONS.ASSERTION_ERROR",
+		                             "CONSTRAINT_ERROR",
+		                             "LZ4ADA.DEVICE_ERROR" };
+	if (status < 0 || status > LZ4ADA_DEVICE_ERROR)
+		return "UNKNOWN";
+	return names[status];
+}
+
+const char* lz4ada_thread_last_error(void) { return g_thread_error.c_str(); }
+
+const char* lz4ada_last_error(const lz4ada_decompressor* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int lz4ada_device_check(void)
+{
+	return guarded(nullptr, [] { device_check_or_raise(); });
+}
+
+void lz4ada_to_hex8(uint8_t v, char out[3]) { snprintf(out, 3, "%02x", v); }
+void lz4ada_to_hex32(uint32_t v, char out[9]) { snprintf(out, 9, "%08x", v); }
+
+int lz4ada_init(int reservation, int64_t* min_buffer_size, lz4ada_decompressor** ctx)
+{
+	*ctx = nullptr;
+	return guarded(nullptr, [&] {  // lz4ada.adb:48-63
+		if (!concrete(reservation))
+			raise(LZ4ADA_CONSTRAINT_ERROR, "Init requires a Memory_Reservation (SZ_*)");
+		const int64_t bmax = block_size_of(reservation);
+		*min_buffer_size = bmax + HISTORY_SIZE + 8;
+		auto* c = new_ctx(bmax + 4 + BLOCK_SIZE_BYTES - 1);
+		c->m.memory_reservation = reservation;
+		*ctx = c;
+	});
+}
+
+int lz4ada_init_with_header(const uint8_t* input, int64_t len, int reservation,
+                            int64_t* num_consumed, int64_t* min_buffer_size,
+                            lz4ada_decompressor** ctx)
+{
+	*ctx = nullptr;
+	*num_consumed = 0;
+	return guarded(nullptr, [&] {  // lz4ada.adb:79-125
+		if (len < 7)
+			raise(LZ4ADA_ASSERTION_ERROR, "failed precondition from lz4ada.ads:243");
+		if (reservation < LZ4ADA_SZ_64_KIB || reservation > LZ4ADA_SINGLE_FRAME)
+			raise(LZ4ADA_CONSTRAINT_ERROR, "bad reservation");
+		uint8_t hb[20];
+		Meta mt;
+		mt.memory_reservation =
+		        reservation == LZ4ADA_SINGLE_FRAME ? int(LZ4ADA_USE_FIRST) : reservation;
+		int64_t pos = 0;
+		while (mt.header_parsing != HDR_DONE) {
+			if (pos >= len)
+				raise(LZ4ADA_TOO_FEW_HEADER_BYTES,
+				      "Expected at least " + img_u(mt.size_remaining) +
+				              " more bytes but header input has already ended.");
+			const int64_t c = header_bytes(mt, hb, input + pos, len - pos);
+			pos += c;
+			*num_consumed += c;
+		}
+		const int64_t bmax = block_size_of(mt.memory_reservation);
+		*min_buffer_size = bmax + HISTORY_SIZE + 8;
+		if (reservation == LZ4ADA_SINGLE_FRAME)
+			mt.memory_reservation = LZ4ADA_SINGLE_FRAME;
+		auto* c = new_ctx(bmax + mt.block_checksum_length + BLOCK_SIZE_BYTES - 1);
+		c->m = mt;
+		*ctx = c;
+	});
+}
+
+int lz4ada_init_for_block(int64_t compressed_length, int reservation, int64_t* min_buffer_size,
+                          lz4ada_decompressor** ctx)
+{
+	*ctx = nullptr;
+	return guarded(nullptr, [&] {  // lz4ada.adb:127-147
+		if (!concrete(reservation))
+			raise(LZ4ADA_CONSTRAINT_ERROR, "Init_For_Block requires a Memory_Reservation");
+		const int64_t bmax = block_size_of(reservation);
+		*min_buffer_size = bmax + HISTORY_SIZE + 8;
+		auto* c = new_ctx(bmax - 1);
+		c->m.is_format = F_BLOCK;
+		c->m.is_compressed = true;
+		c->m.header_parsing = HDR_DONE;
+		c->m.memory_reservation = reservation;
+		c->input_length = compressed_length;
+		*ctx = c;
+	});
+}
+
+int lz4ada_update(lz4ada_decompressor* ctx, const uint8_t* input, int64_t len,
+                  int64_t* num_consumed, uint8_t* buffer, int64_t buffer_len,
+                  int64_t* output_first, int64_t* output_last)
+{
+	*num_consumed = 0;
+	*output_first = 1;
+	*output_last = 0;
+	return guarded(&ctx->err, [&] {
+		ctx->update(input, len, *num_consumed, buffer, buffer_len, *output_first, *output_last);
+	});
+}
+
+int lz4ada_is_end_of_frame(const lz4ada_decompressor* ctx) { return ctx->is_end_of_frame(); }
+
+void lz4ada_free(lz4ada_decompressor* ctx) { delete ctx; }
+
+// -------------------------------------------------------------- XXHash32
+
+void lz4ada_xxh32_reset(lz4ada_xxh32_state* h, uint32_t seed)  // lz4ada.adb:932-940
+{
+	h->state[0] = seed + P1 + P2;
+	h->state[1] = seed + P2;
+	h->state[2] = seed;
+	h->state[3] = seed - P1;
+	memset(h->buffer, 0, sizeof h->buffer);
+	h->buffer_size = 0;
+	h->total_length = 0;
+	h->hash = 0;
+}
+
+void lz4ada_xxh32_init(lz4ada_xxh32_state* h, uint32_t seed)  // :925-930 (Q1)
+{
+	(void)seed;
+	lz4ada_xxh32_reset(h, 0);
+}
+
+static int xxh32_update_dev(lz4ada_xxh32_state* h, const void* d_data, int64_t len,
+                            hipStream_t stream)
+{
+	return guarded(nullptr, [&] {
+		device_check_or_raise();
+		DevBuf<lz4ada_xxh32_state> ds;
+		ds.reserve(1);
+		HIP_OK(hipMemcpyAsync(ds.p, h, sizeof *h, hipMemcpyHostToDevice, stream));
+		HIP_OK(launch_xxh32_update(ds.p, static_cast<const uint8_t*>(d_data), uint64_t(len), stream));
+		HIP_OK(hipMemcpyAsync(h, ds.p, sizeof *h, hipMemcpyDeviceToHost, stream));
+		HIP_OK(hipStreamSynchronize(stream));
+	});
+}
+
+int lz4ada_xxh32_update_device(lz4ada_xxh32_state* h, const void* d_data, int64_t len,
+                               void* stream)
+{
+	return xxh32_update_dev(h, d_data, len, static_cast<hipStream_t>(stream));
+}
+
+int lz4ada_xxh32_update(lz4ada_xxh32_state* h, const uint8_t* data, int64_t len)
+{
+	return guarded(nullptr, [&] {
+		device_check_or_raise();
+		DevBuf<uint8_t> d;
+		d.reserve(size_t(std::max<int64_t>(len, 1)));
+		if (len > 0)
+			HIP_OK(hipMemcpy(d.p, data, size_t(len), hipMemcpyHostToDevice));
+		int st = xxh32_update_dev(h, d.p, len, nullptr);
+		if (st)
+			raise(st, g_thread_error);
+	});
+}
+
+uint32_t lz4ada_xxh32_final(const lz4ada_xxh32_state* h)
+{
+	// Final() is computed on the device by every update; refresh it for a
+	// state that has not seen one yet.
+	lz4ada_xxh32_state t = *h;
+	if (t.total_length == 0 && t.hash == 0) {
+		if (xxh32_update_dev(&t, nullptr, 0, nullptr) != LZ4ADA_OK)
+			return 0;
+	}
+	return t.hash;
+}
+
+int lz4ada_xxh32_hash(const uint8_t* data, int64_t len, uint32_t* out)
+{
+	lz4ada_xxh32_state h;
+	lz4ada_xxh32_init(&h, 0);
+	int st = lz4ada_xxh32_update(&h, data, len);
+	if (st == LZ4ADA_OK)
+		*out = h.hash;
+	return st;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ bulk path
+
+namespace lz4ada {
+
+// Walk one frame's block size words (Try_Detect_Input_Length semantics,
+// lz4ada.adb:525-585, under Init_With_Header(Single_Frame)).
+static void index_frame(const uint8_t* f, int64_t len, lz4ada_frame_info& info,
+                        std::vector<lz4ada_block_desc>* descs)
+{
+	memset(&info, 0, sizeof info);
+	if (len < 7)
+		raise(LZ4ADA_ASSERTION_ERROR, "failed precondition from lz4ada.ads:243");
+	Meta mt;
+	mt.memory_reservation = LZ4ADA_USE_FIRST;
+	uint8_t hb[20];
+	int64_t pos = 0;
+	while (mt.header_parsing != HDR_DONE) {
+		if (pos >= len)
+			raise(LZ4ADA_TOO_FEW_HEADER_BYTES,
+			      "Expected at least " + img_u(mt.size_remaining) +
+			              " more bytes but header input has already ended.");
+		pos += header_bytes(mt, hb, f + pos, len - pos);
+	}
+	info.header_len = pos;
+	const int64_t bmax = block_size_of(mt.memory_reservation);
+	info.block_max = bmax;
+	if (mt.is_format == F_SKIPPABLE) {
+		info.format = LZ4ADA_FORMAT_SKIPPABLE;
+		info.frame_len = pos + int64_t(mt.size_remaining);
+		info.nblocks = 0;
+		return;
+	}
+	info.format = mt.is_format == F_LEGACY ? LZ4ADA_FORMAT_LEGACY : LZ4ADA_FORMAT_MODERN;
+	info.flg = mt.flg;
+	info.bd = mt.bd;
+	info.block_checksum = mt.block_checksum_length ? 1 : 0;
+	info.content_checksum = mt.content_checksum_length ? 1 : 0;
+	info.has_content_size = mt.has_content_size ? 1 : 0;
+	info.independent = (mt.is_format == F_LEGACY) || (mt.flg & 0x20u) ? 1 : 0;
+	info.content_size = mt.has_content_size ? mt.size_remaining : 0;
+	const int64_t inbuf = bmax + mt.block_checksum_length + BLOCK_SIZE_BYTES;
+	const int64_t additional = BLOCK_SIZE_BYTES + mt.block_checksum_length;
+	int64_t nb = 0;
+	for (;;) {
+		if (pos + 4 > len) {
+			if (mt.is_format == F_LEGACY && pos == len)
+				break;  // legacy frames end with the input
+			raise(LZ4ADA_DATA_CORRUPTION, "Frame truncated: block size word missing.");
+		}
+		uint32_t word = load32(f + pos);
+		if (mt.is_format == F_MODERN && word == 0) {
+			pos += 4;
+			if (mt.content_checksum_length) {
+				if (pos + 4 > len)
+					raise(LZ4ADA_DATA_CORRUPTION, "Frame truncated: content checksum missing.");
+				info.content_checksum_declared = load32(f + pos);
+				pos += 4;
+			}
+			break;
+		}
+		if (mt.is_format == F_LEGACY && is_any_magic(word))
+			break;  // next frame starts here
+		bool stored = false;
+		if (mt.is_format == F_MODERN) {
+			stored = (word & 0x80000000u) != 0;
+			word &= 0x7ffffffu;
+		}
+		if (int64_t(word) + additional > inbuf)
+			raise(LZ4ADA_DATA_CORRUPTION,
+			      "Declared maximum data length exceeded. Buffer has " + img(inbuf) +
+			              " bytes, current block requires " + img_u(word) + " bytes + " +
+			              img(additional) + " bytes for metadata.");
+		const int64_t payload = pos + 4;
+		const int64_t end = payload + int64_t(word) + mt.block_checksum_length;
+		if (end > len)
+			raise(LZ4ADA_DATA_CORRUPTION, "Frame truncated inside a block.");
+		if (descs) {
+			lz4ada_block_desc d{};
+			d.in_off = uint64_t(payload);
+			d.in_len = word;
+			d.flags = (stored ? LZ4ADA_BLOCK_STORED : 0u) |
+			          (mt.block_checksum_length ? LZ4ADA_BLOCK_HAS_CKSUM : 0u);
+			d.out_off = uint64_t(nb) * uint64_t(bmax);
+			d.out_cap = uint32_t(bmax);
+			d.cksum = mt.block_checksum_length ? load32(f + payload + word) : 0u;
+			descs->push_back(d);
+		}
+		++nb;
+		pos = end;
+	}
+	info.nblocks = nb;
+	info.frame_len = pos;
+}
+
+// Reference-exact path for one frame: the unlz4ada loop
+// (tool_unlz4ada/unlz4ada.adb:84-103) over the streaming engine.
+static void exact_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out_cap,
+                        int64_t& out_len, int64_t& consumed_total)
+{
+	int64_t consumed = 0, mbs = 0;
+	lz4ada_decompressor* raw = nullptr;
+	int st = lz4ada_init_with_header(f, len, LZ4ADA_SINGLE_FRAME, &consumed, &mbs, &raw);
+	if (st)
+		raise(st, g_thread_error);
+	std::unique_ptr<lz4ada_decompressor> ctx(raw);
+	std::vector<uint8_t> buf(size_t(mbs), 0);
+	out_len = 0;
+	int eof = LZ4ADA_EOF_NO;
+	int64_t pos = consumed;
+	while (pos < len) {
+		int64_t c = 0, first = 1, last = 0;
+		ctx->update(f + pos, len - pos, c, buf.data(), mbs, first, last);
+		if (last >= first) {
+			const int64_t nout = last - first + 1;
+			if (out_len + nout > out_cap)
+				raise(LZ4ADA_CONSTRAINT_ERROR, "output capacity exceeded");
+			memcpy(out + out_len, buf.data() + first, size_t(nout));
+			out_len += nout;
+		}
+		pos += c;
+		eof = ctx->is_end_of_frame();
+		if (eof == LZ4ADA_EOF_YES)
+			break;
+		if (c == 0 && last < first)
+			raise(LZ4ADA_CONSTRAINT_ERROR, "decoder made no progress");
+	}
+	if (eof == LZ4ADA_EOF_NO)
+		raise(LZ4ADA_CONSTRAINT_ERROR, "End not signalled by library. Unable to process all data");
+	consumed_total = pos;
+}
+
+// Fast path: every block on its own wavefront.  Returns false when the
+// frame needs the exact path (any block status, checksum mismatch,
+// oversize or short block layouts the slots cannot express).
+static bool fast_frame(const uint8_t* f, int64_t len, const lz4ada_frame_info& info,
+                       const std::vector<lz4ada_block_desc>& descs, uint8_t* out,
+                       int64_t out_cap, int64_t& out_len)
+{
+	device_check_or_raise();
+	hipStream_t stream = nullptr;
+	const uint32_t nb = uint32_t(descs.size());
+	DevBuf<uint8_t> d_frame, d_out;
+	DevBuf<lz4ada_block_desc> d_desc;
+	DevBuf<lz4ada_block_status> d_st;
+	d_frame.reserve(size_t(info.frame_len));
+	HIP_OK(hipMemcpy(d_frame.p, f, size_t(info.frame_len), hipMemcpyHostToDevice));
+	const uint64_t slots = uint64_t(std::max<uint32_t>(nb, 1)) * uint64_t(info.block_max);
+	d_out.reserve(size_t(slots));
+	d_desc.reserve(std::max<uint32_t>(nb, 1));
+	d_st.reserve(std::max<uint32_t>(nb, 1));
+	if (nb) {
+		HIP_OK(hipMemcpy(d_desc.p, descs.data(), nb * sizeof(lz4ada_block_desc),
+		                 hipMemcpyHostToDevice));
+		HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
+		HIP_OK(launch_block_checksums(d_frame.p, d_desc.p, nb, d_st.p, stream));
+		HIP_OK(launch_decode_blocks(d_frame.p, uint64_t(info.frame_len), d_desc.p, nb, d_out.p,
+		                            d_st.p, stream));
+	}
+	std::vector<lz4ada_block_status> st(nb);
+	if (nb)
+		HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status),
+		                 hipMemcpyDeviceToHost));
+	uint64_t total = 0;
+	bool contiguous = true;
+	std::vector<uint64_t> dst_off(nb);
+	for (uint32_t i = 0; i < nb; ++i) {
+		if (st[i].code != DS_OK)
+			return false;
+		if ((descs[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != descs[i].cksum)
+			return false;
+		dst_off[i] = total;
+		if (total != descs[i].out_off)
+			contiguous = false;
+		total += st[i].out_len;
+	}
+	if (info.has_content_size && total != info.content_size)
+		return false;
+	if (int64_t(total) > out_cap)
+		raise(LZ4ADA_CONSTRAINT_ERROR, "output capacity exceeded");
+	const uint8_t* d_res = d_out.p;
+	DevBuf<uint8_t> d_compact;
+	if (!contiguous) {
+		DevBuf<uint64_t> d_off;
+		d_off.reserve(nb);
+		d_compact.reserve(size_t(std::max<uint64_t>(total, 1)));
+		HIP_OK(hipMemcpy(d_off.p, dst_off.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice));
+		HIP_OK(launch_compact(d_out.p, d_desc.p, d_off.p, d_st.p, nb, d_compact.p, stream));
+		HIP_OK(hipDeviceSynchronize());
+		d_res = d_compact.p;
+	}
+	if (info.content_checksum) {
+		lz4ada_xxh32_state h;
+		lz4ada_xxh32_reset(&h, 0);
+		DevBuf<lz4ada_xxh32_state> d_h;
+		d_h.reserve(1);
+		HIP_OK(hipMemcpy(d_h.p, &h, sizeof h, hipMemcpyHostToDevice));
+		HIP_OK(launch_xxh32_update(d_h.p, d_res, total, stream));
+		HIP_OK(hipMemcpy(&h, d_h.p, sizeof h, hipMemcpyDeviceToHost));
+		if (h.hash != info.content_checksum_declared)
+			return false;
+	}
+	if (total)
+		HIP_OK(hipMemcpy(out, d_res, size_t(total), hipMemcpyDeviceToHost));
+	out_len = int64_t(total);
+	return true;
+}
+
+static void decode_one_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out_cap,
+                             int64_t& out_len, int64_t& consumed)
+{
+	lz4ada_frame_info info;
+	std::vector<lz4ada_block_desc> descs;
+	bool indexed = true;
+	try {
+		index_frame(f, len, info, &descs);
+	} catch (const Error&) {
+		indexed = false;  // the exact path raises the reference's error in order
+	}
+	if (indexed && info.format == LZ4ADA_FORMAT_SKIPPABLE && info.frame_len <= len) {
+		out_len = 0;  // Skip (lz4ada.adb:420-433): nothing to decode
+		consumed = info.frame_len;
+		return;
+	}
+	if (indexed && info.format == LZ4ADA_FORMAT_MODERN && info.independent &&
+	    info.frame_len <= len) {
+		if (fast_frame(f, len, info, descs, out, out_cap, out_len)) {
+			consumed = info.frame_len;
+			return;
+		}
+	}
+	// A legacy frame has no end mark: it ends where the next magic starts
+	// (what tool_unlz4ada's per-frame re-init achieves), so hand the exact
+	// path only this frame's bytes.
+	const int64_t flen = (indexed && info.format == LZ4ADA_FORMAT_LEGACY) ? info.frame_len : len;
+	exact_frame(f, flen, out, out_cap, out_len, consumed);
+}
+
+}  // namespace lz4ada
+
+extern "C" {
+
+int lz4ada_frame_index(const uint8_t* frame, int64_t len, lz4ada_frame_info* info,
+                       lz4ada_block_desc* descs, int64_t desc_cap)
+{
+	return guarded(nullptr, [&] {
+		std::vector<lz4ada_block_desc> v;
+		index_frame(frame, len, *info, descs ? &v : nullptr);
+		if (descs) {
+			if (int64_t(v.size()) > desc_cap)
+				raise(LZ4ADA_CONSTRAINT_ERROR, "descriptor capacity exceeded");
+			memcpy(descs, v.data(), v.size() * sizeof(lz4ada_block_desc));
+		}
+	});
+}
+
+int lz4ada_launch_decode(const void* d_frame, uint64_t frame_len, const lz4ada_block_desc* d_descs,
+                         int64_t nblocks, void* d_out, lz4ada_block_status* d_status, void* stream)
+{
+	return guarded(nullptr, [&] {
+		HIP_OK(launch_decode_blocks(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
+		                            uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,
+		                            static_cast<hipStream_t>(stream)));
+	});
+}
+
+int lz4ada_launch_block_checksums(const void* d_frame, const lz4ada_block_desc* d_descs,
+                                  int64_t nblocks, lz4ada_block_status* d_status, void* stream)
+{
+	return guarded(nullptr, [&] {
+		HIP_OK(launch_block_checksums(static_cast<const uint8_t*>(d_frame), d_descs,
+		                              uint32_t(nblocks), d_status,
+		                              static_cast<hipStream_t>(stream)));
+	});
+}
+
+int lz4ada_decode_blocks_device(const void* d_frame, uint64_t frame_len,
+                                const lz4ada_block_desc* d_descs, int64_t nblocks, void* d_out,
+                                lz4ada_block_status* d_status, void* stream)
+{
+	return guarded(nullptr, [&] {
+		hipStream_t s = static_cast<hipStream_t>(stream);
+		HIP_OK(launch_block_checksums(static_cast<const uint8_t*>(d_frame), d_descs,
+		                              uint32_t(nblocks), d_status, s));
+		HIP_OK(launch_decode_blocks(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
+		                            uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status, s));
+	});
+}
+
+int lz4ada_output_checksums_device(const void* d_out, const lz4ada_block_desc* d_descs,
+                                   const lz4ada_block_status* d_status, int64_t nblocks,
+                                   uint32_t* d_hash, void* stream)
+{
+	return guarded(nullptr, [&] {
+		HIP_OK(launch_output_checksums(static_cast<const uint8_t*>(d_out), d_descs,
+		                               uint32_t(nblocks), d_status, d_hash,
+		                               static_cast<hipStream_t>(stream)));
+	});
+}
+
+int lz4ada_decode_frame(const uint8_t* frame, int64_t len, uint8_t* out, int64_t out_cap,
+                        int64_t* out_len, int64_t* frame_consumed)
+{
+	*out_len = 0;
+	*frame_consumed = 0;
+	return guarded(nullptr, [&] { decode_one_frame(frame, len, out, out_cap, *out_len, *frame_consumed); });
+}
+
+int lz4ada_decode_stream(const uint8_t* input, int64_t len, uint8_t* out, int64_t out_cap,
+                         int64_t* out_len)
+{
+	*out_len = 0;
+	return guarded(nullptr, [&] {
+		int64_t pos = 0;
+		while (pos < len) {
+			int64_t n = 0, c = 0;
+			decode_one_frame(input + pos, len - pos, out + *out_len, out_cap - *out_len, n, c);
+			*out_len += n;
+			if (c <= 0)
+				raise(LZ4ADA_CONSTRAINT_ERROR, "decoder made no progress");
+			pos += c;
+		}
+	});
+}
+
+int64_t lz4ada_decoded_bound(const uint8_t* input, int64_t len)
+{
+	int64_t pos = 0, bound = 0;
+	while (pos < len) {
+		lz4ada_frame_info info;
+		if (lz4ada_frame_index(input + pos, len - pos, &info, nullptr, 0) != LZ4ADA_OK)
+			return -1;
+		if (info.frame_len <= 0)
+			return -1;
+		bound += info.nblocks * info.block_max;
+		pos += info.frame_len;
+	}
+	return bound;
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// lz4ada_internal.h -- types shared by the host frame engine (lz4ada_host.cpp)
+// and the gfx950 kernels (lz4ada_kernels.hip).  Not part of the public C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lz4ada_hip.h"
+
+namespace lz4ada {
+
+// XXH32 primes (lz4ada.ads:323-328).
+constexpr uint32_t P1 = 2654435761u;
+constexpr uint32_t P2 = 2246822519u;
+constexpr uint32_t P3 = 3266489917u;
+constexpr uint32_t P4 = 668265263u;
+constexpr uint32_t P5 = 374761393u;
+
+constexpr int64_t HISTORY_SIZE = 65536;  // lz4ada.ads:350
+constexpr int64_t BLOCK_SIZE_BYTES = 4;  // lz4ada.ads:351
+
+// Device status codes written by the decode kernels (per block).
+enum DevStatus : int32_t {
+	DS_OK = 0,
+	DS_OFFSET0 = 1,        // lz4ada.adb:769-772
+	DS_ML_AFTER_LIT = 2,   // lz4ada.adb:752-762 (aux = Match_Length nibble)
+	DS_LIT_OVERRUN = 3,    // D3
+	DS_TRUNCATED = 4,      // D4
+	DS_OUT_OVERFLOW = 5,   // D5 (bulk: block_max slot; serial: Buffer)
+	DS_PRE_BLOCK_REF = 6,  // back-reference before the block start (bulk)
+	DS_BACKREF = 7,        // lz4ada.adb:867-874 (detail = H_Offset)
+	DS_CONTENT_SIZE = 8,   // lz4ada.adb:830-835
+};
+
+// State of the serial reference-exact block kernel (emulates one
+// Decode_Full_Block_With_Trailer step on a device mirror of Buffer).
+struct SerialState {
+	int64_t output_pos;          // Ctx.Output_Pos
+	int64_t output_pos_history;  // Ctx.Output_Pos_History
+	int64_t first, last;         // Output_First / Output_Last
+	uint64_t size_remaining;     // Ctx.M.Size_Remaining
+	int32_t has_content_size;
+	int32_t code;   // DevStatus
+	int32_t aux;
+	int32_t pad;
+	int64_t detail;
+};
+
+// ---- launchers (lz4ada_kernels.hip) ----
+// All launch on `stream` and never synchronise.
+
+// Bulk independent-block decode: one wavefront per block.
+hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
+                                const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                uint8_t* d_out, lz4ada_block_status* d_status,
+                                hipStream_t stream);
+
+// Per-block XXH32 of the compressed payloads (block checksums).
+hipError_t launch_block_checksums(const uint8_t* d_frame,
+                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                  lz4ada_block_status* d_status, hipStream_t stream);
+
+// Per-block XXH32 of decoded output slots (golden checks).
+hipError_t launch_output_checksums(const uint8_t* d_out,
+                                   const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                   const lz4ada_block_status* d_status,
+                                   uint32_t* d_hash, hipStream_t stream);
+
+// Streaming XXH32 update of a device-resident state over device data.
+// Also refreshes state->hash with the Final() value.
+hipError_t launch_xxh32_update(lz4ada_xxh32_state* d_state, const uint8_t* d_data,
+                               uint64_t len, hipStream_t stream);
+
+// Reference-exact serial decode of one block into the Buffer mirror.
+hipError_t launch_serial_block(uint8_t* d_buf, int64_t buflen, const uint8_t* d_blk,
+                               int64_t raw_len, int64_t data_len, int compressed,
+                               SerialState* d_state, hipStream_t stream);
+
+// Gather variable-length slots into a contiguous buffer (short blocks).
+hipError_t launch_compact(const uint8_t* d_src, const lz4ada_block_desc* d_desc,
+                          const uint64_t* d_dst_off, const lz4ada_block_status* d_status,
+                          uint32_t nblocks, uint8_t* d_dst, hipStream_t stream);
+
+}  // namespace lz4ada

@@ -1,0 +1,391 @@
+"""lz4ada -- Python host binding of the MI355X-native LZ4Ada decompressor.
+
+Mirrors the reference's public Ada package (lib/lz4ada.ads) over the C-ABI
+in include/lz4ada_hip.h, loaded with ctypes from the in-tree
+bo-lz4-ada_amd/liblz4ada_hip.so:
+
+    LZ4Ada.Init / Init_With_Header / Init_For_Block   -> Decompressor.init*
+    LZ4Ada.Update / Is_End_Of_Frame                   -> Decompressor.update / is_end_of_frame
+    LZ4Ada.XXHash32.Init/Reset/Update/Final/Hash      -> XXHash32
+    Checksum_Error, Data_Corruption, Not_Supported,
+    Too_Few_Header_Bytes, Too_Little_Memory           -> exceptions of the same names
+
+Every block byte is decoded on the GPU; there is no CPU fallback.  Importing
+fails loudly when the shared library is missing; decoding fails with
+DeviceError when no GPU is usable.
+"""
+import ctypes
+import enum
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblz4ada_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is missing: build it with `make -C bo-lz4-ada_amd/csrc` "
+                      "or __graft_entry__.build() (no CPU fallback exists)")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_i64 = ctypes.c_int64
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+
+
+class Reservation(enum.IntEnum):
+    """Flexible_Memory_Reservation (lz4ada.ads:79-106)."""
+    SZ_64_KiB = 0
+    SZ_256_KiB = 1
+    SZ_1_MiB = 2
+    SZ_4_MiB = 3
+    SZ_8_MiB = 4
+    Use_First = 5
+    Single_Frame = 6
+
+
+FOR_MODERN = Reservation.SZ_4_MiB   # lz4ada.ads:92
+FOR_LEGACY = Reservation.SZ_8_MiB   # lz4ada.ads:100
+FOR_ALL = Reservation.SZ_8_MiB      # lz4ada.ads:106
+
+
+class EndOfFrame(enum.IntEnum):
+    """End_Of_Frame (lz4ada.ads:124)."""
+    Yes = 0
+    No = 1
+    Maybe = 2
+
+
+# ------------------------------------------------------------------ errors
+
+class LZ4AdaError(Exception):
+    """Base: str() is the reference's Exception_Information line."""
+    ada_name = "LZ4ADA.ERROR"
+
+    def __init__(self, message: str):
+        super().__init__(message)
+        self.message = message
+
+    def __str__(self):
+        return f"raised {self.ada_name} : {self.message}"
+
+
+class ChecksumError(LZ4AdaError):
+    ada_name = "LZ4ADA.CHECKSUM_ERROR"
+
+
+class DataCorruption(LZ4AdaError):
+    ada_name = "LZ4ADA.DATA_CORRUPTION"
+
+
+class NotSupported(LZ4AdaError):
+    ada_name = "LZ4ADA.NOT_SUPPORTED"
+
+
+class TooFewHeaderBytes(LZ4AdaError):
+    ada_name = "LZ4ADA.TOO_FEW_HEADER_BYTES"
+
+
+class TooLittleMemory(LZ4AdaError):
+    ada_name = "LZ4ADA.TOO_LITTLE_MEMORY"
+
+
+class AssertionFailure(LZ4AdaError):
+    ada_name = "ADA.ASSERTIONS.ASSERTION_ERROR"
+
+
+class ConstraintError(LZ4AdaError):
+    ada_name = "CONSTRAINT_ERROR"
+
+
+class DeviceError(LZ4AdaError):
+    ada_name = "LZ4ADA.DEVICE_ERROR"
+
+
+_ERRORS = {1: ChecksumError, 2: DataCorruption, 3: NotSupported, 4: TooFewHeaderBytes,
+           5: TooLittleMemory, 6: AssertionFailure, 7: ConstraintError, 8: DeviceError}
+
+
+def _check(status: int, message: str):
+    if status:
+        raise _ERRORS.get(status, LZ4AdaError)(message)
+
+
+def _thread_error() -> str:
+    return _lib.lz4ada_thread_last_error().decode()
+
+
+# ---------------------------------------------------------------- signatures
+
+class BlockDesc(ctypes.Structure):
+    _fields_ = [("in_off", ctypes.c_uint64), ("in_len", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("out_off", ctypes.c_uint64),
+                ("out_cap", ctypes.c_uint32), ("cksum", ctypes.c_uint32)]
+
+
+class BlockStatus(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("aux", ctypes.c_int32), ("detail", ctypes.c_int64),
+                ("err_out_pos", ctypes.c_int64), ("out_len", ctypes.c_uint32),
+                ("cksum", ctypes.c_uint32)]
+
+
+class FrameInfo(ctypes.Structure):
+    _fields_ = [("format", ctypes.c_int32), ("flg", ctypes.c_uint8), ("bd", ctypes.c_uint8),
+                ("block_checksum", ctypes.c_uint8), ("content_checksum", ctypes.c_uint8),
+                ("has_content_size", ctypes.c_uint8), ("independent", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 2), ("block_max", ctypes.c_int64),
+                ("header_len", ctypes.c_int64), ("nblocks", ctypes.c_int64),
+                ("frame_len", ctypes.c_int64), ("content_size", ctypes.c_uint64),
+                ("content_checksum_declared", ctypes.c_uint32), ("pad2", ctypes.c_uint32)]
+
+
+class XXH32State(ctypes.Structure):
+    _fields_ = [("state", ctypes.c_uint32 * 4), ("buffer", ctypes.c_uint8 * 16),
+                ("buffer_size", ctypes.c_int32), ("hash", ctypes.c_uint32),
+                ("total_length", ctypes.c_uint64)]
+
+
+BLOCK_STORED = 1
+BLOCK_HAS_CKSUM = 2
+FORMAT_MODERN, FORMAT_LEGACY, FORMAT_SKIPPABLE = 1, 2, 3
+
+_P = ctypes.POINTER
+_sig = {
+    "lz4ada_abi_version": ([], ctypes.c_int),
+    "lz4ada_device_check": ([], ctypes.c_int),
+    "lz4ada_error_name": ([ctypes.c_int], ctypes.c_char_p),
+    "lz4ada_thread_last_error": ([], ctypes.c_char_p),
+    "lz4ada_last_error": ([_vp], ctypes.c_char_p),
+    "lz4ada_init": ([ctypes.c_int, _pi64, _P(_vp)], ctypes.c_int),
+    "lz4ada_init_with_header": ([_vp, _i64, ctypes.c_int, _pi64, _pi64, _P(_vp)], ctypes.c_int),
+    "lz4ada_init_for_block": ([_i64, ctypes.c_int, _pi64, _P(_vp)], ctypes.c_int),
+    "lz4ada_update": ([_vp, _vp, _i64, _pi64, _vp, _i64, _pi64, _pi64], ctypes.c_int),
+    "lz4ada_is_end_of_frame": ([_vp], ctypes.c_int),
+    "lz4ada_free": ([_vp], None),
+    "lz4ada_to_hex8": ([ctypes.c_uint8, ctypes.c_char_p], None),
+    "lz4ada_to_hex32": ([ctypes.c_uint32, ctypes.c_char_p], None),
+    "lz4ada_xxh32_init": ([_P(XXH32State), ctypes.c_uint32], None),
+    "lz4ada_xxh32_reset": ([_P(XXH32State), ctypes.c_uint32], None),
+    "lz4ada_xxh32_update": ([_P(XXH32State), _vp, _i64], ctypes.c_int),
+    "lz4ada_xxh32_update_device": ([_P(XXH32State), _vp, _i64, _vp], ctypes.c_int),
+    "lz4ada_xxh32_final": ([_P(XXH32State)], ctypes.c_uint32),
+    "lz4ada_xxh32_hash": ([_vp, _i64, _P(ctypes.c_uint32)], ctypes.c_int),
+    "lz4ada_frame_index": ([_vp, _i64, _P(FrameInfo), _vp, _i64], ctypes.c_int),
+    "lz4ada_decode_blocks_device": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp],
+                                    ctypes.c_int),
+    "lz4ada_launch_decode": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp], ctypes.c_int),
+    "lz4ada_launch_block_checksums": ([_vp, _vp, _i64, _vp, _vp], ctypes.c_int),
+    "lz4ada_output_checksums_device": ([_vp, _vp, _vp, _i64, _vp, _vp], ctypes.c_int),
+    "lz4ada_decode_frame": ([_vp, _i64, _vp, _i64, _pi64, _pi64], ctypes.c_int),
+    "lz4ada_decode_stream": ([_vp, _i64, _vp, _i64, _pi64], ctypes.c_int),
+    "lz4ada_decoded_bound": ([_vp, _i64], _i64),
+    "lz4ada_gen_block": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _vp, _i64], _i64),
+}
+for _name, (_args, _res) in _sig.items():
+    _f = getattr(_lib, _name)
+    _f.argtypes = _args
+    _f.restype = _res
+
+EXPORTED = tuple(_sig)
+
+
+def _addr(obj, offset=0):
+    """Address of a bytes / bytearray / memoryview / ctypes buffer (+offset)."""
+    if obj is None:
+        return None
+    if isinstance(obj, bytes):
+        return ctypes.cast(ctypes.c_char_p(obj), _vp).value + offset
+    if isinstance(obj, (bytearray, memoryview)):
+        mv = memoryview(obj)
+        if mv.readonly:
+            obj = bytes(mv)
+            return ctypes.cast(ctypes.c_char_p(obj), _vp).value + offset
+        if mv.nbytes == 0:
+            return None
+        return ctypes.addressof(ctypes.c_char.from_buffer(mv)) + offset
+    return ctypes.addressof(obj) + offset
+
+
+def device_available() -> bool:
+    return _lib.lz4ada_device_check() == 0
+
+
+def error_name(status: int) -> str:
+    return _lib.lz4ada_error_name(status).decode()
+
+
+def to_hex(num: int, width: int = 32) -> str:
+    """LZ4Ada.To_Hex (lz4ada.ads:306-307)."""
+    if width == 8:
+        b = ctypes.create_string_buffer(3)
+        _lib.lz4ada_to_hex8(num, b)
+    else:
+        b = ctypes.create_string_buffer(9)
+        _lib.lz4ada_to_hex32(num, b)
+    return b.value.decode()
+
+
+# ------------------------------------------------------------ Decompressor
+
+class Decompressor:
+    """LZ4Ada.Decompressor (lz4ada.ads:126).  Caller owns `buffer`."""
+
+    def __init__(self, ptr: int):
+        self._p = _vp(ptr)
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p is not None and p.value:
+            _lib.lz4ada_free(p)
+            self._p = None
+
+    @classmethod
+    def init(cls, reservation=FOR_ALL):
+        """Init (lz4ada.ads:218-220) -> (ctx, min_buffer_size)."""
+        mbs, p = _i64(), _vp()
+        _check(_lib.lz4ada_init(int(reservation), ctypes.byref(mbs), ctypes.byref(p)),
+               _thread_error())
+        return cls(p.value), mbs.value
+
+    @classmethod
+    def init_with_header(cls, data, reservation=Reservation.Single_Frame):
+        """Init_With_Header (lz4ada.ads:238-243) -> (ctx, num_consumed, min_buffer_size)."""
+        cons, mbs, p = _i64(), _i64(), _vp()
+        st = _lib.lz4ada_init_with_header(_addr(data), len(data), int(reservation),
+                                          ctypes.byref(cons), ctypes.byref(mbs), ctypes.byref(p))
+        _check(st, _thread_error())
+        return cls(p.value), cons.value, mbs.value
+
+    @classmethod
+    def init_for_block(cls, compressed_length: int, reservation=FOR_ALL):
+        """Init_For_Block (lz4ada.ads:255-258) -> (ctx, min_buffer_size)."""
+        mbs, p = _i64(), _vp()
+        _check(_lib.lz4ada_init_for_block(compressed_length, int(reservation),
+                                          ctypes.byref(mbs), ctypes.byref(p)), _thread_error())
+        return cls(p.value), mbs.value
+
+    def update(self, data, buffer, start: int = 0, stop=None):
+        """Update (lz4ada.ads:281-287) on data[start:stop] ->
+        (num_consumed, output_first, output_last); output is buffer[first:last+1]."""
+        stop = len(data) if stop is None else stop
+        n = stop - start
+        cons, first, last = _i64(), _i64(), _i64()
+        st = _lib.lz4ada_update(self._p, _addr(data, start) if n > 0 else None, n,
+                                ctypes.byref(cons), _addr(buffer), len(buffer),
+                                ctypes.byref(first), ctypes.byref(last))
+        if st:
+            _check(st, _lib.lz4ada_last_error(self._p).decode())
+        return cons.value, first.value, last.value
+
+    def is_end_of_frame(self) -> EndOfFrame:
+        return EndOfFrame(_lib.lz4ada_is_end_of_frame(self._p))
+
+
+# ---------------------------------------------------------------- XXHash32
+
+class XXHash32:
+    """LZ4Ada.XXHash32 (lz4ada.ads:311-344); lanes advance on the GPU."""
+
+    def __init__(self, seed: int = 0):
+        self._s = XXH32State()
+        _lib.lz4ada_xxh32_init(ctypes.byref(self._s), seed)  # seed ignored (Q1)
+
+    def reset(self, seed: int = 0):
+        _lib.lz4ada_xxh32_reset(ctypes.byref(self._s), seed)
+
+    def update(self, data):
+        _check(_lib.lz4ada_xxh32_update(ctypes.byref(self._s), _addr(data), len(data)),
+               _thread_error())
+
+    def update_device(self, d_ptr: int, length: int, stream: int = 0):
+        _check(_lib.lz4ada_xxh32_update_device(ctypes.byref(self._s), d_ptr, length, stream),
+               _thread_error())
+
+    def final(self) -> int:
+        return _lib.lz4ada_xxh32_final(ctypes.byref(self._s))
+
+    @staticmethod
+    def hash(data) -> int:
+        out = ctypes.c_uint32()
+        _check(_lib.lz4ada_xxh32_hash(_addr(data), len(data), ctypes.byref(out)),
+               _thread_error())
+        return out.value
+
+
+# ------------------------------------------------------------- bulk decode
+
+def frame_index(data, offset: int = 0):
+    """Host frame indexer -> (FrameInfo, ctypes array of BlockDesc)."""
+    info = FrameInfo()
+    n = len(data) - offset
+    _check(_lib.lz4ada_frame_index(_addr(data, offset), n, ctypes.byref(info), None, 0),
+           _thread_error())
+    descs = (BlockDesc * max(info.nblocks, 1))()
+    _check(_lib.lz4ada_frame_index(_addr(data, offset), n, ctypes.byref(info), descs,
+                                   info.nblocks), _thread_error())
+    return info, descs
+
+
+def decoded_bound(data) -> int:
+    return _lib.lz4ada_decoded_bound(_addr(data), len(data))
+
+
+def decode_frame(data, offset: int = 0):
+    """One frame (Single_Frame semantics) -> (decoded bytes, bytes consumed)."""
+    n = len(data) - offset
+    bound = _lib.lz4ada_decoded_bound(_addr(data, offset), n)
+    cap = max(bound, 0) + (64 << 10)
+    out = ctypes.create_string_buffer(max(cap, 1))
+    olen, cons = _i64(), _i64()
+    _check(_lib.lz4ada_decode_frame(_addr(data, offset), n, out, cap, ctypes.byref(olen),
+                                    ctypes.byref(cons)), _thread_error())
+    return out.raw[:olen.value], cons.value
+
+
+def decode_stream(data) -> bytes:
+    """Every frame of a concatenated stream -> decoded bytes."""
+    bound = _lib.lz4ada_decoded_bound(_addr(data), len(data))
+    cap = max(bound, 0) + (64 << 10)
+    out = ctypes.create_string_buffer(max(cap, 1))
+    olen = _i64()
+    _check(_lib.lz4ada_decode_stream(_addr(data), len(data), out, cap, ctypes.byref(olen)),
+           _thread_error())
+    return out.raw[:olen.value]
+
+
+def decode_blocks_device(d_frame: int, frame_len: int, d_descs: int, nblocks: int, d_out: int,
+                         d_status: int, stream: int = 0):
+    """Launch block checksums + decode over device-resident buffers (async)."""
+    _check(_lib.lz4ada_decode_blocks_device(d_frame, frame_len, d_descs, nblocks, d_out,
+                                            d_status, stream), _thread_error())
+
+
+def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=0):
+    _check(_lib.lz4ada_launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status,
+                                     stream), _thread_error())
+
+
+def launch_block_checksums(d_frame, d_descs, nblocks, d_status, stream=0):
+    _check(_lib.lz4ada_launch_block_checksums(d_frame, d_descs, nblocks, d_status, stream),
+           _thread_error())
+
+
+def output_checksums_device(d_out, d_descs, d_status, nblocks, d_hash, stream=0):
+    _check(_lib.lz4ada_output_checksums_device(d_out, d_descs, d_status, nblocks, d_hash,
+                                               stream), _thread_error())
+
+
+# ---------------------------------------------------------- synthetic data
+
+GEN_DENSE, GEN_MIXED, GEN_RLE, GEN_LITERAL = 0, 1, 2, 3
+GEN_KINDS = {"dense": GEN_DENSE, "mixed": GEN_MIXED, "rle": GEN_RLE, "literal": GEN_LITERAL}
+
+
+def gen_block(kind: int, seed: int, raw_len: int):
+    """One synthetic compressed block -> (payload bytes, decoded bytes)."""
+    raw = ctypes.create_string_buffer(max(raw_len, 1))
+    cap = raw_len + raw_len // 128 + 64 + raw_len // 200 + 1024
+    comp = ctypes.create_string_buffer(cap)
+    n = _lib.lz4ada_gen_block(kind, seed, raw, raw_len, comp, cap)
+    if n < 0:
+        raise RuntimeError("gen_block: capacity")
+    return comp.raw[:n], raw.raw[:raw_len]

@@ -1,0 +1,255 @@
+/*
+ * lz4ada_hip.h -- C-ABI of the MI355X-native LZ4Ada decompressor.
+ *
+ * Drop-in boundary for the reference's public Ada API (lib/lz4ada.ads):
+ * every entry point below names the reference subprogram it replaces.  An
+ * Ada caller binds them with pragma Import (bindings/ada/lz4ada_hip.ads,
+ * INTEGRATION.md); Python binds them with ctypes (bo-lz4-ada_amd/lz4ada.py).
+ *
+ * Plain pointers and sizes only.  Lengths are int64_t so that both the
+ * Integer and the Stream_Element_Offset overloads map onto one entry point.
+ * Status codes are 1:1 with the reference's exceptions (lz4ada.ads:133-162);
+ * the exact Exception_Information message is available from
+ * lz4ada_last_error() / lz4ada_thread_last_error().
+ *
+ * Block decode, block/content XXH32 and the XXHash32 API run on the GPU
+ * (HIP kernels for gfx950).  Frame-header parsing and the Update state
+ * machine are host code.  There is no CPU fallback: without a usable GPU,
+ * calls that would decode return LZ4ADA_DEVICE_ERROR.
+ */
+#ifndef LZ4ADA_HIP_H
+#define LZ4ADA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LZ4ADA_HIP_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- enums */
+
+/* Exceptions (lz4ada.ads:133-162). */
+typedef enum {
+	LZ4ADA_OK = 0,
+	LZ4ADA_CHECKSUM_ERROR = 1,       /* LZ4Ada.Checksum_Error */
+	LZ4ADA_DATA_CORRUPTION = 2,      /* LZ4Ada.Data_Corruption */
+	LZ4ADA_NOT_SUPPORTED = 3,        /* LZ4Ada.Not_Supported */
+	LZ4ADA_TOO_FEW_HEADER_BYTES = 4, /* LZ4Ada.Too_Few_Header_Bytes */
+	LZ4ADA_TOO_LITTLE_MEMORY = 5,    /* LZ4Ada.Too_Little_Memory */
+	LZ4ADA_ASSERTION_ERROR = 6,      /* Pre/Assert violated (API misuse) */
+	LZ4ADA_CONSTRAINT_ERROR = 7,     /* library-internal check */
+	LZ4ADA_DEVICE_ERROR = 8          /* HIP error / no GPU (no reference twin) */
+} lz4ada_status;
+
+/* Flexible_Memory_Reservation (lz4ada.ads:79-106), same order. */
+typedef enum {
+	LZ4ADA_SZ_64_KIB = 0,
+	LZ4ADA_SZ_256_KIB = 1,
+	LZ4ADA_SZ_1_MIB = 2,
+	LZ4ADA_SZ_4_MIB = 3,
+	LZ4ADA_SZ_8_MIB = 4,
+	LZ4ADA_USE_FIRST = 5,
+	LZ4ADA_SINGLE_FRAME = 6,
+	LZ4ADA_FOR_MODERN = LZ4ADA_SZ_4_MIB, /* lz4ada.ads:92 */
+	LZ4ADA_FOR_LEGACY = LZ4ADA_SZ_8_MIB, /* lz4ada.ads:100 */
+	LZ4ADA_FOR_ALL = LZ4ADA_SZ_8_MIB     /* lz4ada.ads:106 */
+} lz4ada_reservation;
+
+/* End_Of_Frame (lz4ada.ads:124). */
+typedef enum { LZ4ADA_EOF_YES = 0, LZ4ADA_EOF_NO = 1, LZ4ADA_EOF_MAYBE = 2 } lz4ada_end_of_frame;
+
+/* ------------------------------------------------- streaming decompressor */
+
+/* Opaque Decompressor context (lz4ada.ads:126, 440-449).  Owns device
+ * buffers (Buffer mirror holding the 64 KiB history, block staging, content
+ * hash state); not copyable; one thread at a time. */
+typedef struct lz4ada_decompressor lz4ada_decompressor;
+
+/* LZ4Ada.Init (lz4ada.ads:189-191, 218-220; lz4ada.adb:48-63).
+ * reservation: one of LZ4ADA_SZ_*. */
+int lz4ada_init(int reservation, int64_t *min_buffer_size, lz4ada_decompressor **ctx);
+
+/* LZ4Ada.Init_With_Header (lz4ada.ads:238-243; lz4ada.adb:79-125).
+ * Requires len >= 7 (Pre).  On failure *ctx is NULL and the message is in
+ * lz4ada_thread_last_error(). */
+int lz4ada_init_with_header(const uint8_t *input, int64_t len, int reservation,
+                            int64_t *num_consumed, int64_t *min_buffer_size,
+                            lz4ada_decompressor **ctx);
+
+/* LZ4Ada.Init_For_Block (lz4ada.ads:255-258; lz4ada.adb:127-147). */
+int lz4ada_init_for_block(int64_t compressed_length, int reservation,
+                          int64_t *min_buffer_size, lz4ada_decompressor **ctx);
+
+/* LZ4Ada.Update (lz4ada.ads:211-216, 281-287; lz4ada.adb:383-418).
+ * buffer is the caller-owned 0-based Buffer (length >= min_buffer_size);
+ * it must not be modified between calls.  At most one block of output is
+ * returned, as inclusive indices [*output_first, *output_last]
+ * (first = 1, last = 0 when nothing was produced). */
+int lz4ada_update(lz4ada_decompressor *ctx, const uint8_t *input, int64_t len,
+                  int64_t *num_consumed, uint8_t *buffer, int64_t buffer_len,
+                  int64_t *output_first, int64_t *output_last);
+
+/* LZ4Ada.Is_End_Of_Frame (lz4ada.ads:303; lz4ada.adb:906-915). */
+int lz4ada_is_end_of_frame(const lz4ada_decompressor *ctx);
+
+/* Exception message of the last failed call on ctx, and the reference
+ * exception name for a status ("LZ4ADA.DATA_CORRUPTION"). */
+const char *lz4ada_last_error(const lz4ada_decompressor *ctx);
+const char *lz4ada_error_name(int status);
+/* Message of the last failed context-less call on this thread. */
+const char *lz4ada_thread_last_error(void);
+
+void lz4ada_free(lz4ada_decompressor *ctx);
+
+/* LZ4Ada.To_Hex (lz4ada.ads:306-307); writes 3 / 9 bytes incl. NUL. */
+void lz4ada_to_hex8(uint8_t v, char out[3]);
+void lz4ada_to_hex32(uint32_t v, char out[9]);
+
+/* ---------------------------------------------------------------- XXHash32 */
+
+/* LZ4Ada.XXHash32.Hasher (lz4ada.ads:335-343).  Plain struct so callers can
+ * embed it; the lanes are advanced on the GPU.  `hash` caches Final(). */
+typedef struct {
+	uint32_t state[4];
+	uint8_t buffer[16];
+	int32_t buffer_size;
+	uint32_t hash;
+	uint64_t total_length;
+} lz4ada_xxh32_state;
+
+/* XXHash32.Init (lz4ada.adb:925-930): Seed is ignored (quirk Q1). */
+void lz4ada_xxh32_init(lz4ada_xxh32_state *h, uint32_t seed);
+/* XXHash32.Reset (lz4ada.adb:932-940). */
+void lz4ada_xxh32_reset(lz4ada_xxh32_state *h, uint32_t seed);
+/* XXHash32.Update (lz4ada.adb:942-963) over host bytes. */
+int lz4ada_xxh32_update(lz4ada_xxh32_state *h, const uint8_t *data, int64_t len);
+/* Same over device-resident bytes; stream is a hipStream_t (0 = default). */
+int lz4ada_xxh32_update_device(lz4ada_xxh32_state *h, const void *d_data, int64_t len,
+                               void *stream);
+/* XXHash32.Final (lz4ada.adb:993-1017). */
+uint32_t lz4ada_xxh32_final(const lz4ada_xxh32_state *h);
+/* XXHash32.Hash (lz4ada.adb:1019-1024), seed 0, host bytes. */
+int lz4ada_xxh32_hash(const uint8_t *data, int64_t len, uint32_t *out);
+
+/* ------------------------------------------------------- bulk frame decode */
+/*
+ * The hot path.  A whole LZ4 frame is indexed on the host (a serial walk of
+ * the 4-byte block size words, lz4ada.adb:525-585) and every block is then
+ * decoded by its own wavefront on the GPU, with block checksums
+ * (lz4ada.adb:698-707) verified on the GPU.  Output lands in per-block
+ * slots of block_max bytes (desc.out_off), contiguous whenever every
+ * non-last block is full.  A non-zero block status, a failed checksum, a
+ * back-reference before its block start (linked / B.Indep=0 data) or an
+ * oversize block sends lz4ada_decode_frame() down the reference-exact
+ * serial path, which reproduces the reference's output and exception.
+ */
+
+typedef struct {
+	uint64_t in_off;  /* payload offset inside the frame */
+	uint32_t in_len;  /* payload bytes (size word & 0x7FFFFFF) */
+	uint32_t flags;   /* LZ4ADA_BLOCK_* */
+	uint64_t out_off; /* output slot offset */
+	uint32_t out_cap; /* slot capacity (block_max) */
+	uint32_t cksum;   /* declared block checksum (if present) */
+} lz4ada_block_desc;
+
+#define LZ4ADA_BLOCK_STORED 1u    /* size word bit 31 set */
+#define LZ4ADA_BLOCK_HAS_CKSUM 2u /* FLG.B.Checksum */
+
+typedef struct {
+	int32_t code;        /* 0 = ok; else device status */
+	int32_t aux;
+	int64_t detail;
+	int64_t err_out_pos; /* block-relative output count at the error */
+	uint32_t out_len;    /* decoded bytes */
+	uint32_t cksum;      /* XXH32 of the compressed payload */
+} lz4ada_block_status;
+
+#define LZ4ADA_FORMAT_MODERN 1
+#define LZ4ADA_FORMAT_LEGACY 2
+#define LZ4ADA_FORMAT_SKIPPABLE 3
+
+typedef struct {
+	int32_t format;           /* LZ4ADA_FORMAT_* */
+	uint8_t flg, bd;          /* frame descriptor bytes (modern) */
+	uint8_t block_checksum;   /* FLG bit 4 */
+	uint8_t content_checksum; /* FLG bit 2 */
+	uint8_t has_content_size; /* FLG bit 3 */
+	uint8_t independent;      /* FLG bit 5 (B.Indep; ignored by the reference) */
+	uint8_t pad[2];
+	int64_t block_max;        /* BD block maximum (8 MiB for legacy) */
+	int64_t header_len;
+	int64_t nblocks;
+	int64_t frame_len;        /* bytes of this frame incl. end mark + checksum */
+	uint64_t content_size;
+	uint32_t content_checksum_declared;
+	uint32_t pad2;
+} lz4ada_frame_info;
+
+/* Index one frame starting at frame[0].  descs may be NULL to count blocks
+ * (then info->nblocks is set and LZ4ADA_OK returned).  Slots are laid out
+ * at i * block_max.  Errors carry the reference's header messages. */
+int lz4ada_frame_index(const uint8_t *frame, int64_t len, lz4ada_frame_info *info,
+                       lz4ada_block_desc *descs, int64_t desc_cap);
+
+/* Launch the per-block kernels over a device-resident frame: block XXH32
+ * (when LZ4ADA_BLOCK_HAS_CKSUM) and decode into d_out.  Asynchronous on
+ * `stream` (hipStream_t).  d_frame must stay readable up to frame_len. */
+int lz4ada_decode_blocks_device(const void *d_frame, uint64_t frame_len,
+                                const lz4ada_block_desc *d_descs, int64_t nblocks,
+                                void *d_out, lz4ada_block_status *d_status,
+                                void *stream);
+
+/* Decode-only / checksum-only halves of the above (for profiling). */
+int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
+                         const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
+                         lz4ada_block_status *d_status, void *stream);
+int lz4ada_launch_block_checksums(const void *d_frame, const lz4ada_block_desc *d_descs,
+                                  int64_t nblocks, lz4ada_block_status *d_status,
+                                  void *stream);
+
+/* XXH32 of each decoded slot (golden checks). */
+int lz4ada_output_checksums_device(const void *d_out, const lz4ada_block_desc *d_descs,
+                                   const lz4ada_block_status *d_status, int64_t nblocks,
+                                   uint32_t *d_hash, void *stream);
+
+/* Decode one complete single frame (Init_With_Header(Single_Frame) + Update
+ * semantics, as tool_unlz4ada does per frame) from host memory into host
+ * memory.  *frame_consumed = bytes of this frame; *out_len = decoded bytes.
+ * On failure the reference's exception message is in
+ * lz4ada_thread_last_error().  out_cap must be >= the decoded size. */
+int lz4ada_decode_frame(const uint8_t *frame, int64_t len, uint8_t *out, int64_t out_cap,
+                        int64_t *out_len, int64_t *frame_consumed);
+
+/* Decode every frame of a concatenated stream (skippable frames skipped). */
+int lz4ada_decode_stream(const uint8_t *input, int64_t len, uint8_t *out, int64_t out_cap,
+                         int64_t *out_len);
+
+/* Upper bound of the decoded size of a stream (sum of block maxima). */
+int64_t lz4ada_decoded_bound(const uint8_t *input, int64_t len);
+
+/* ------------------------------------------------------------------ misc */
+
+/* 0 when a HIP device is usable, else LZ4ADA_DEVICE_ERROR (message in
+ * lz4ada_thread_last_error()). */
+int lz4ada_device_check(void);
+int lz4ada_abi_version(void);
+
+/*
+ * Deterministic synthetic LZ4 block generator for benches and tests
+ * (SURVEY §8d): emits one valid compressed block whose decoded size is
+ * exactly raw_len.  kind: 0 dense (~5 B/sequence), 1 mixed (~32 B/seq,
+ * ratio ~2), 2 rle (zeros, offset 1), 3 literal-heavy.  Writes the decoded
+ * bytes to raw (raw_len bytes) and the block payload to comp; returns the
+ * payload length, or -1 if comp_cap is too small.
+ */
+int64_t lz4ada_gen_block(int kind, uint64_t seed, uint8_t *raw, int64_t raw_len,
+                         uint8_t *comp, int64_t comp_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,226 @@
+"""GPU parity tests: the MI355X decoder (through its C-ABI) against the
+reference's fixtures and the CPU oracle.  Mirrors test_suite/lz4test.adb.
+"""
+import hashlib
+import random
+
+import pytest
+
+import _oracle as O
+from conftest import error_vectors, good_vectors, read_eds, read_vector
+
+import lz4ada
+import lz4frame
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not lz4ada.device_available():
+        pytest.fail("MI355X not usable: " + lz4ada._thread_error())
+
+
+def feed(ctx, mbs, data, chunk):
+    """lz4test.adb:32-83 (Test_Good_Case_Inner) over the product."""
+    buf = bytearray(mbs)
+    out = bytearray()
+    pos = 0
+    eof = ctx.is_end_of_frame()
+    while pos < len(data):
+        win_end = min(pos + chunk, len(data))
+        used = pos
+        while used < win_end:
+            c, f, l = ctx.update(data, buf, used, win_end)
+            if l >= f:
+                out += buf[f:l + 1]
+            used += c
+            eof = ctx.is_end_of_frame()
+        pos = win_end
+    return bytes(out), eof
+
+
+def check_digest(out, want):
+    assert len(out) == want["len"]
+    assert hashlib.sha256(out).hexdigest() == want["sha256"]
+
+
+@pytest.mark.parametrize("chunk", [4096, 1], ids=["4K", "1b"])
+@pytest.mark.parametrize("name", good_vectors())
+def test_good_vector_streaming(name, chunk, digests):
+    data = read_vector(name, "lz4")
+    if chunk == 1 and len(data) > 1_000_000:
+        chunk = 7  # keeps the per-byte Python loop bounded; still splits every block
+    ctx, mbs = lz4ada.Decompressor.init(lz4ada.FOR_ALL)
+    out, eof = feed(ctx, mbs, data, chunk)
+    assert eof != lz4ada.EndOfFrame.No
+    check_digest(out, digests[name])
+
+
+@pytest.mark.parametrize("name", good_vectors())
+def test_good_vector_bulk(name, digests):
+    data = read_vector(name, "lz4")
+    out = lz4ada.decode_stream(data)
+    check_digest(out, digests[name])
+
+
+def test_xxh32_individual_bytes():
+    tc = bytes([0x1a] * 14 + [0x11, 0x10])
+    h = lz4ada.XXHash32()
+    for b in tc:
+        h.update(bytes([b]))
+    assert h.final() == 0xf994ef8a
+    assert lz4ada.XXHash32.hash(tc) == 0xf994ef8a
+
+
+def test_xxh32_random_against_oracle():
+    rng = random.Random(3)
+    for n in [0, 1, 15, 16, 17, 255, 256, 1023, 1024, 1025, 4096 + 3, 100_000, 1 << 20]:
+        data = rng.randbytes(n + 7)
+        for off in (0, 1, 3):
+            chunk = data[off:off + n]
+            assert lz4ada.XXHash32.hash(chunk) == O.xxh32(chunk), (n, off)
+    h = lz4ada.XXHash32()
+    data = rng.randbytes(50_000)
+    i = 0
+    while i < len(data):
+        k = rng.randint(1, 3000)
+        h.update(data[i:i + k])
+        i += k
+    assert h.final() == O.xxh32(data)
+
+
+def test_decompress_individual_bytes():
+    # lz4test.adb:149-214
+    tc = bytes.fromhex(
+        "02214c1830000000f01f3c3f786d6c2076657273696f6e3d22312e302220656e636f"
+        "64696e673d225554462d38223f3e3c746573742f3e0a02214c180e000000d048656c"
+        "6c6f20776f726c642e0a")
+    expect = b'<?xml version="1.0" encoding="UTF-8"?><test/>\nHello world.\n'
+    ctx, consumed, mbs = lz4ada.Decompressor.init_with_header(tc, lz4ada.FOR_ALL)
+    buf = bytearray(mbs)
+    have = b""
+    for i in range(consumed, len(tc)):
+        nc = 0
+        while nc == 0:
+            nc, f, l = ctx.update(tc, buf, i, i + 1)
+            assert not (nc == 0 and l < f)
+            if l >= f:
+                have += bytes(buf[f:l + 1])
+    assert have == expect
+
+
+def test_hello_block():
+    # lz4test.adb:216-248
+    tc = bytes.fromhex("d048656c6c6f2c20776f726c642e")
+    ctx, mbs = lz4ada.Decompressor.init_for_block(len(tc))
+    buf = bytearray(mbs)
+    c, f, l = ctx.update(tc, buf)
+    assert c == len(tc)
+    assert ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes
+    assert bytes(buf[:13]) == b"Hello, world."
+
+
+def error_harness(data):
+    """lz4test.adb:280-308 over the product."""
+    ctx, total, mbs = lz4ada.Decompressor.init_with_header(data, lz4ada.Reservation.Single_Frame)
+    buf = bytearray(mbs)
+    while total < len(data):
+        c, f, l = ctx.update(data, buf, total)
+        assert c != 0, "No more data accepted but no exception signalled"
+        total += c
+    raise AssertionError("All data processed but no exception raised")
+
+
+@pytest.mark.parametrize("name", error_vectors())
+def test_error_vector(name):
+    data = read_vector(name, "err")[:10001]
+    with pytest.raises(lz4ada.LZ4AdaError) as ei:
+        error_harness(data)
+    assert str(ei.value) == read_eds(name)
+
+
+def test_unexpected_multi_frame():
+    tc = read_vector("minilegacy", "lz4") * 2
+    with pytest.raises(lz4ada.DataCorruption):
+        error_harness(tc)
+
+
+# ------------------------------------------------ synthetic frames (bulk)
+
+def synth_frame(kind, nblocks, block_max, seed=0, last_short=True, block_cksum=True,
+                content_cksum=True, indep=True, stored_every=0):
+    blocks = []
+    for i in range(nblocks):
+        raw_len = block_max
+        if last_short and i == nblocks - 1:
+            raw_len = block_max // 3 + 17
+        if stored_every and i % stored_every == stored_every - 1:
+            raw = random.Random(seed + i).randbytes(raw_len)
+            blocks.append((raw, raw, True))
+        else:
+            comp, raw = lz4ada.gen_block(kind, seed * 1000 + i, raw_len)
+            blocks.append((comp, raw, False))
+    return lz4frame.build_frame(blocks, block_max, indep=indep, block_cksum=block_cksum,
+                                content_cksum=content_cksum)
+
+
+@pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
+@pytest.mark.parametrize("block_max", [64 << 10, 4 << 20])
+def test_synthetic_independent_frame(kind, block_max):
+    nb = 6 if block_max == 64 << 10 else 3
+    frame, raw = synth_frame(lz4ada.GEN_KINDS[kind], nb, block_max, seed=5, stored_every=4)
+    out, consumed = lz4ada.decode_frame(frame)
+    assert consumed == len(frame)
+    assert out == raw
+    st, oref, eof, msg = O.decode_stream(frame)
+    assert st == O.OK and oref == raw
+
+
+def test_synthetic_short_middle_blocks_compact():
+    # non-last blocks shorter than block_max force the compaction pass
+    blocks = []
+    for i, n in enumerate([1000, 65536, 5, 40000, 65536, 777]):
+        comp, raw = lz4ada.gen_block(i % 4, 77 + i, n)
+        blocks.append((comp, raw, False))
+    frame, raw = lz4frame.build_frame(blocks, 64 << 10, block_cksum=True, content_cksum=True)
+    out, _ = lz4ada.decode_frame(frame)
+    assert out == raw
+
+
+def test_bulk_errors_fall_back_to_exact_messages():
+    frame, raw = synth_frame(0, 4, 64 << 10, seed=9)
+    # flip a byte inside block 2's payload -> its block checksum fails
+    info, descs = lz4ada.frame_index(frame)
+    bad = bytearray(frame)
+    bad[descs[2].in_off + 100] ^= 0x55
+    with pytest.raises(lz4ada.ChecksumError) as ei:
+        lz4ada.decode_frame(bytes(bad))
+    st, msg = O.error_harness(bytes(bad))
+    assert str(ei.value) == O.exception_information(st, msg)
+
+
+def test_device_resident_blocks():
+    torch = pytest.importorskip("torch")
+    import ctypes
+    frame, raw = synth_frame(1, 8, 64 << 10, seed=11, stored_every=3)
+    info, descs = lz4ada.frame_index(frame)
+    nb = info.nblocks
+    dev = torch.device("cuda:0")
+    d_frame = torch.frombuffer(bytearray(frame), dtype=torch.uint8).to(dev)
+    d_desc = torch.frombuffer(bytearray(bytes(descs)[:nb * 32]), dtype=torch.uint8).to(dev)
+    d_out = torch.zeros(nb * info.block_max, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
+    d_hash = torch.zeros(nb, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    lz4ada.decode_blocks_device(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
+                                d_out.data_ptr(), d_st.data_ptr(), stream)
+    torch.cuda.synchronize()
+    st = (lz4ada.BlockStatus * nb).from_buffer_copy(d_st.cpu().numpy().tobytes())
+    total = sum(s.out_len for s in st)
+    assert total == len(raw)
+    assert all(s.code == 0 for s in st)
+    for i in range(nb):
+        if descs[i].flags & lz4ada.BLOCK_HAS_CKSUM:
+            assert st[i].cksum == descs[i].cksum
+    assert bytes(d_out.cpu().numpy()[:total]) == raw
