@@ -1,0 +1,313 @@
+#!/usr/bin/env python3
+"""bench.py -- MI355X LZ4Ada decode throughput (BASELINE.json metric).
+
+One step = the hot path over one batch: every block of this rank's shard of
+a synthetic 4 MiB-block independent frame goes through the GPU block
+checksum (XXH32 of each compressed payload, lz4ada.adb:698-707) and the
+GPU block decoder (lz4ada.adb:716-904), input already resident in HBM,
+output left in HBM.
+
+Workload (config.workload): BASELINE.json configs[3] shape -- 4 MiB blocks,
+FLG 0x70 (version 01 | B.Indep | B.Checksum), BD 0x70 (4 MiB) -- with a
+fixed shard of 2048 blocks (8 GiB decoded, the size of configs[2]) per GPU,
+so N GPUs decode an N x 8 GiB frame (weak scaling; N = 4 is configs[3]'s
+32 GiB).  The frame has no content checksum, so nothing is skipped; the
+content-checksum variant (configs[2], FLG 0x74) is reported separately as
+`e2e_content_checksum` because a frame-wide XXH32 is one serial chain
+(SURVEY §7 H2).
+
+Synthetic data: 64 unique blocks from the repo's deterministic LZ4
+sequence generator (seed 0x4C5A3441 + i), tiled to size on the device.
+Golden check: per-block XXH32 of every decoded slot (on the GPU) against
+the generator's plaintext hash, after the warmup.
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL); blocks shard
+across ranks with no data-path collective.  Timing: barrier +
+synchronize on both sides of exactly K steps, max over ranks.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bo-lz4-ada_amd"))
+
+import torch  # noqa: E402  (load torch's HIP runtime before liblz4ada_hip.so)
+import torch.distributed as dist  # noqa: E402
+import xxhash  # noqa: E402
+
+import lz4ada  # noqa: E402
+import lz4frame  # noqa: E402
+
+METRIC = "decompressed MiB/s + achieved HBM GB/s vs roofline, 4MiB-block frame @1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SEED0 = 0x4C5A3441
+MiB = 1 << 20
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def make_unique_blocks(kind, n_unique, block_max):
+    """-> list of (record bytes incl. size word + checksum, payload len, raw len, raw xxh32)."""
+    recs = []
+    for i in range(n_unique):
+        comp, raw = lz4ada.gen_block(kind, SEED0 + i, block_max)
+        rec = lz4frame.block_record(comp, stored=False, block_cksum=True)
+        recs.append((rec, len(comp), len(raw), xxhash.xxh32(raw).intdigest(), comp, raw))
+    return recs
+
+
+def build_shard(recs, first_block, nblocks, block_max, dev):
+    """Tile the unique block records into this rank's shard of the frame."""
+    n_unique = len(recs)
+    order = [(first_block + i) % n_unique for i in range(nblocks)]
+    offs, pos = [], 0
+    for u in order:
+        offs.append(pos)
+        pos += len(recs[u][0])
+    frame_len = pos + 64
+    d_frame = torch.empty(frame_len, dtype=torch.uint8, device=dev)
+    d_frame[pos:].zero_()
+    d_unique = [torch.frombuffer(bytearray(r[0]), dtype=torch.uint8).to(dev) for r in recs]
+    for i, u in enumerate(order):
+        d_frame[offs[i]:offs[i] + len(recs[u][0])].copy_(d_unique[u])
+    descs = (lz4ada.BlockDesc * nblocks)()
+    exp_hash = []
+    comp_bytes = raw_bytes = 0
+    for i, u in enumerate(order):
+        rec, clen, rlen, h = recs[u][:4]
+        d = descs[i]
+        d.in_off = offs[i] + 4
+        d.in_len = clen
+        d.flags = lz4ada.BLOCK_HAS_CKSUM
+        d.out_off = i * block_max
+        d.out_cap = block_max
+        d.cksum = int.from_bytes(rec[4 + clen:8 + clen], "little")
+        exp_hash.append(h)
+        comp_bytes += clen
+        raw_bytes += rlen
+    d_desc = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+    torch.cuda.synchronize()
+    del d_unique
+    return d_frame, frame_len, d_desc, exp_hash, comp_bytes, raw_bytes, descs
+
+
+def check_statuses(d_status, nblocks):
+    st = (lz4ada.BlockStatus * nblocks).from_buffer_copy(d_status.cpu().numpy().tobytes())
+    return st
+
+
+def cpu_baseline(recs, block_max, budget_s):
+    """The oracle (lz4ada.adb restated in C, 'port') through the reference's
+    CLI loop (tool_unlz4ada: 4 KiB reads, one Update per call), one core,
+    on a bounded prefix of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    def frame_of(k):
+        blocks = [(recs[i % len(recs)][4], recs[i % len(recs)][5], False) for i in range(k)]
+        return lz4frame.build_frame(blocks, block_max, indep=True, block_cksum=True)
+    f1, raw1 = frame_of(1)
+    t0 = time.perf_counter()
+    st, out, msg = O.unlz4ada(f1, out_cap=len(raw1) + MiB)
+    t1 = time.perf_counter() - t0
+    assert st == O.OK and out == raw1, msg
+    k = max(1, min(len(recs) * 4, int(budget_s / max(t1, 1e-6))))
+    fk, rawk = frame_of(k)
+    t0 = time.perf_counter()
+    st, out, msg = O.unlz4ada(fk, out_cap=len(rawk) + MiB)
+    dt = time.perf_counter() - t0
+    assert st == O.OK and len(out) == len(rawk), msg
+    return {"value": round(len(rawk) / dt / MiB, 1), "unit": "MiB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{k} x 4 MiB blocks ({len(rawk) / MiB:.0f} MiB decoded, {dt:.1f} s) of the "
+                      "same frame through the oracle's unlz4ada loop (4 KiB reads, Update per "
+                      "call, block checksums verified)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kind", default="mixed", choices=sorted(lz4ada.GEN_KINDS))
+    ap.add_argument("--blocks-per-gpu", type=int, default=2048)
+    ap.add_argument("--block-max", type=int, default=4 * MiB)
+    ap.add_argument("--unique", type=int, default=64)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--classes", default="", help="extra classes to time, e.g. dense,rle,literal")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_decode.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    nb = args.blocks_per_gpu
+    bmax = args.block_max
+    kind = lz4ada.GEN_KINDS[args.kind]
+    log(f"[bench] generating {args.unique} unique {args.kind} blocks ...")
+    recs = make_unique_blocks(kind, args.unique, bmax)
+    d_frame, frame_len, d_desc, exp_hash, comp_bytes, raw_bytes, descs = build_shard(
+        recs, rank * nb, nb, bmax, dev)
+    d_out = torch.empty(nb * bmax, dtype=torch.uint8, device=dev)
+    d_status = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
+    d_hash = torch.zeros(nb, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    fp, dp, op, sp = d_frame.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), d_status.data_ptr()
+    log(f"[bench] shard: {nb} blocks, {comp_bytes / MiB:.0f} MiB compressed -> "
+        f"{raw_bytes / MiB:.0f} MiB decoded")
+
+    def step(events=None):
+        if events is None:
+            lz4ada.decode_blocks_device(fp, frame_len, dp, nb, op, sp, sh)
+            return
+        e0, e1, e2 = events
+        e0.record(stream)
+        lz4ada.launch_block_checksums(fp, dp, nb, sp, sh)
+        e1.record(stream)
+        lz4ada.launch_decode(fp, frame_len, dp, nb, op, sp, sh)
+        e2.record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # ---- golden check (outside the timed region)
+    st = check_statuses(d_status, nb)
+    bad = [i for i in range(nb) if st[i].code != 0 or st[i].cksum != descs[i].cksum]
+    assert not bad, f"block status / checksum errors: {bad[:5]}"
+    lz4ada.output_checksums_device(op, dp, sp, nb, d_hash.data_ptr(), sh)
+    torch.cuda.synchronize()
+    got = [h & 0xffffffff for h in d_hash.cpu().tolist()]
+    assert got == exp_hash, "decoded output differs from the generator's plaintext"
+    assert sum(s.out_len for s in st) == raw_bytes
+    log("[bench] golden check passed (per-block XXH32 of output, block checksums)")
+
+    # ---- timed region: exactly K steps
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed)
+    ck_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / args.steps
+    dec_ms = sum(b.elapsed_time(c) for _, b, c in evs) / args.steps
+    st = check_statuses(d_status, nb)
+    assert all(s.code == 0 for s in st)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    total_raw = raw_bytes * world * args.steps
+    value = total_raw / elapsed / MiB
+    alg_bytes = comp_bytes + raw_bytes  # compressed read once + output written once
+    achieved = alg_bytes / (dec_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc):
+        with open(args.pmc) as fh:
+            pmc = json.load(fh)
+        if pmc.get("config") == {"kind": args.kind, "blocks": nb, "block_max": bmax}:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "kernel": "k_decode_blocks", "kernel_ms": round(dec_ms, 3),
+            "alg_bytes_per_launch": alg_bytes,
+            "checksum_kernel": "k_block_checksums", "checksum_kernel_ms": round(ck_ms, 3)}
+
+    result = {
+        "metric": METRIC, "value": round(value, 1), "unit": "MiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: repo LZ4 sequence generator, 64 unique blocks tiled on device",
+        "config": {"workload": "configs[3] shape per GPU: 4 MiB independent blocks, FLG 0x70 "
+                               "(B.Indep|B.Checksum), BD 0x70; 2048 blocks = 8 GiB decoded "
+                               "per GPU (configs[2] size)",
+                   "class": args.kind, "blocks_per_gpu": nb, "block_max": bmax,
+                   "compressed_bytes_per_gpu": comp_bytes, "decoded_bytes_per_gpu": raw_bytes,
+                   "parallelism": f"block-shard x{world}"},
+        "hbm_gbps_step": round((comp_bytes + raw_bytes) * world / (elapsed / args.steps) / 1e9, 1),
+        "roofline": roof,
+    }
+
+    # ---- configs[2] e2e: + frame-wide content XXH32 (one serial chain)
+    if not args.no_e2e and rank == 0:
+        h = lz4ada.XXHash32()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h.update_device(op, raw_bytes, sh)
+        t_hash = time.perf_counter() - t0
+        result["e2e_content_checksum"] = {
+            "workload": "configs[2]: same 8 GiB frame with FLG 0x74 (+C.Checksum)",
+            "content_xxh32_s": round(t_hash, 3),
+            "value": round(raw_bytes / (ms_per_step * 1e-3 + t_hash) / MiB, 1), "unit": "MiB/s",
+            "note": "frame-wide XXH32 is one serial 4-lane chain (SURVEY H2), run by one "
+                    "wavefront after the decode"}
+
+    # ---- other content classes (fewer steps)
+    extra = {}
+    for cls in [c for c in args.classes.split(",") if c]:
+        recs_c = make_unique_blocks(lz4ada.GEN_KINDS[cls], min(args.unique, 16), bmax)
+        fr, fl, de, eh, cb, rb, _ = build_shard(recs_c, rank * nb, nb, bmax, dev)
+        fpc, dpc = fr.data_ptr(), de.data_ptr()
+        lz4ada.decode_blocks_device(fpc, fl, dpc, nb, op, sp, sh)
+        torch.cuda.synchronize()
+        stc = check_statuses(d_status, nb)
+        assert all(s.code == 0 for s in stc), cls
+        lz4ada.output_checksums_device(op, dpc, sp, nb, d_hash.data_ptr(), sh)
+        torch.cuda.synchronize()
+        assert [h & 0xffffffff for h in d_hash.cpu().tolist()] == eh, cls
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 3
+        e0.record(stream)
+        for _ in range(reps):
+            lz4ada.launch_decode(fpc, fl, dpc, nb, op, sp, sh)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        extra[cls] = {"decode_ms": round(ms, 3), "MiB_s": round(rb / (ms * 1e-3) / MiB, 1),
+                      "frac": round((cb + rb) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                      "ratio": round(cb / rb, 4)}
+        del fr, de
+    if extra:
+        result["classes_decode_kernel"] = extra
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(recs, bmax, args.cpu_budget)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -18,6 +18,15 @@ import ctypes
 import enum
 import os
 
+# PyTorch-ROCm ships its own libamdhip64.so.7 / libhsa-runtime64.so.1.  Two
+# HIP runtimes cannot share a GPU inside one process, so when torch is
+# installed it is loaded first and liblz4ada_hip.so binds to torch's runtime
+# (same SONAME): torch device pointers, streams and RCCL then work with it.
+try:  # pragma: no cover - depends on the image
+    import torch  # noqa: F401
+except Exception:  # torch is optional for this binding
+    torch = None
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblz4ada_hip.so")
 
