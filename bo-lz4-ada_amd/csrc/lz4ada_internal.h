@@ -30,6 +30,7 @@ enum DevStatus : int32_t {
 	DS_PRE_BLOCK_REF = 6,  // back-reference before the block start (bulk)
 	DS_BACKREF = 7,        // lz4ada.adb:867-874 (detail = H_Offset)
 	DS_CONTENT_SIZE = 8,   // lz4ada.adb:830-835
+	DS_INTERNAL = 9,       // decoder invariant broken (never expected)
 };
 
 // State of the serial reference-exact block kernel (emulates one

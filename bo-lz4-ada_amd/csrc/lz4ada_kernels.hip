@@ -35,6 +35,26 @@
 
 namespace lz4ada {
 
+// Device code addresses HBM through address_space(1) pointers so that every
+// access is a global_* instruction (a generic pointer becomes flat_*, which
+// also ticks lgkmcnt and forces extra waits).
+#define GLOBAL __attribute__((address_space(1)))
+typedef const GLOBAL uint8_t cg8;
+typedef GLOBAL uint8_t g8;
+typedef const GLOBAL uint32_t cg32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <class T>
+__device__ __forceinline__ const GLOBAL T* gptr(const T* p)
+{
+	return (const GLOBAL T*)(p);
+}
+template <class T>
+__device__ __forceinline__ GLOBAL T* gptr(T* p)
+{
+	return (GLOBAL T*)(p);
+}
+
 // ------------------------------------------------------------------ XXH32
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r)
@@ -47,22 +67,10 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 // Unaligned little-endian dword from global memory.  Reads only the aligned
 // dwords that contain wanted bytes, so it never touches a page the data
 // does not.
-__device__ __forceinline__ uint32_t ld32u(const uint8_t* p)
+__device__ __forceinline__ uint32_t ld32u_cached(cg8* p)
 {
 	uintptr_t a = reinterpret_cast<uintptr_t>(p);
-	const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-	uint32_t sh = uint32_t(a & 3u);
-	uint32_t lo = __builtin_nontemporal_load(q);
-	if (sh == 0)
-		return lo;
-	uint32_t hi = __builtin_nontemporal_load(q + 1);
-	return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
-
-__device__ __forceinline__ uint32_t ld32u_cached(const uint8_t* p)
-{
-	uintptr_t a = reinterpret_cast<uintptr_t>(p);
-	const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+	cg32* q = reinterpret_cast<cg32*>(a & ~uintptr_t(3));
 	uint32_t sh = uint32_t(a & 3u);
 	uint32_t lo = q[0];
 	if (sh == 0)
@@ -71,38 +79,98 @@ __device__ __forceinline__ uint32_t ld32u_cached(const uint8_t* p)
 	return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-// Advance the four XXH32 accumulators over `nstripes` 16-byte stripes at p.
-// Whole-wave call; lane l carries accumulator (l & 3); every lane returns
-// its (l & 3) accumulator.  (Process, lz4ada.adb:979-991.)
-__device__ uint32_t wave_xxh32_stripes(uint32_t acc, const uint8_t* p, uint64_t nstripes)
+constexpr int XR = 16;  // dwords per lane per step (4 KiB per wave)
+
+// Load step w0's raw dwords: word w of the stream starts at byte 4w, `sh`
+// bytes into aligned dword q[w].  With sh != 0 a word straddles q[w] and
+// q[w+1], both holding wanted bytes (no overread).  The alignbyte happens
+// at use, so the loads stay in flight.
+template <bool MIS, bool GUARD>
+__device__ __forceinline__ void xxh_load(uint32_t (&lo)[XR], uint32_t (&hi)[XR], cg32* q,
+                                         uint64_t w0, uint64_t nwords)
 {
 	const uint32_t lane = lane_id();
+#pragma unroll
+	for (int r = 0; r < XR; ++r) {
+		const uint64_t w = w0 + uint64_t(r) * 64 + lane;
+		const uint64_t wl = (!GUARD || w < nwords) ? w : 0;
+		lo[r] = __builtin_nontemporal_load(q + wl);
+		if (MIS)
+			hi[r] = __builtin_nontemporal_load(q + wl + 1);
+	}
+}
+
+// 16 chain steps over the stripes held in one register of the step.
+__device__ __forceinline__ uint32_t xxh_chain16(uint32_t acc, uint32_t word, int64_t limit)
+{
+	const uint32_t lane = lane_id();
+	const uint32_t prod = word * P2;
+	uint32_t xs[16];
+#pragma unroll
+	for (int k = 0; k < 16; ++k)
+		xs[k] = __shfl(prod, 4 * k + int(lane & 3u));
+	if (limit >= 16) {
+#pragma unroll
+		for (int k = 0; k < 16; ++k)
+			acc = rotl32(acc + xs[k], 13) * P1;
+	} else {
+#pragma unroll
+		for (int k = 0; k < 16; ++k)
+			if (k < limit)
+				acc = rotl32(acc + xs[k], 13) * P1;
+	}
+	return acc;
+}
+
+template <bool MIS>
+__device__ uint32_t xxh32_stripes_impl(uint32_t acc, cg32* q, uint32_t sh, uint64_t nstripes)
+{
 	const uint64_t nwords = nstripes * 4;
-	for (uint64_t w0 = 0; w0 < nwords; w0 += 256) {
-		uint32_t prod[4];
+	constexpr uint64_t STEP = 64 * XR;
+	const uint64_t full = nwords / STEP * STEP;  // words covered by whole steps
+	uint32_t clo[XR], chi[XR], nlo[XR], nhi[XR];
+	if (full)
+		xxh_load<MIS, false>(clo, chi, q, 0, nwords);
+	for (uint64_t w0 = 0; w0 < full; w0 += STEP) {
+		// issue the next step's loads first; they land while the chain runs
+		if (w0 + STEP < full)
+			xxh_load<MIS, false>(nlo, nhi, q, w0 + STEP, nwords);
 #pragma unroll
-		for (int r = 0; r < 4; ++r) {
-			uint64_t w = w0 + uint64_t(r) * 64 + lane;
-			uint32_t word = 0;
-			if (w < nwords)
-				word = ld32u(p + 4 * w);
-			prod[r] = word * P2;
+		for (int r = 0; r < XR; ++r) {
+			const uint32_t word = MIS ? __builtin_amdgcn_alignbyte(chi[r], clo[r], sh) : clo[r];
+			acc = xxh_chain16(acc, word, 16);
 		}
-		const uint64_t left = (nwords - w0) / 4;  // stripes left from w0
 #pragma unroll
-		for (int r = 0; r < 4; ++r) {
-			uint32_t xs[16];
+		for (int r = 0; r < XR; ++r) {
+			clo[r] = nlo[r];
+			if (MIS)
+				chi[r] = nhi[r];
+		}
+	}
+	if (full < nwords) {  // ragged last step
+		xxh_load<MIS, true>(clo, chi, q, full, nwords);
+		const int64_t left = int64_t((nwords - full) / 4);
 #pragma unroll
-			for (int k = 0; k < 16; ++k)
-				xs[k] = __shfl(prod[r], 4 * k + int(lane & 3u));
-#pragma unroll
-			for (int k = 0; k < 16; ++k) {
-				if (uint64_t(r) * 16 + k < left)
-					acc = rotl32(acc + xs[k], 13) * P1;
-			}
+		for (int r = 0; r < XR; ++r) {
+			const uint32_t word = MIS ? __builtin_amdgcn_alignbyte(chi[r], clo[r], sh) : clo[r];
+			acc = xxh_chain16(acc, word, left - 16 * r);
 		}
 	}
 	return acc;
+}
+
+// Advance the four XXH32 accumulators over `nstripes` 16-byte stripes at p
+// (Process, lz4ada.adb:979-991).  Whole-wave call; lane l carries
+// accumulator (l & 3).  The chain is serial: all 64 lanes load 4 KiB per
+// step one step ahead of it, and ds_bpermute hands stripe k's four
+// pre-multiplied words to lanes 0-3.
+__device__ uint32_t wave_xxh32_stripes(uint32_t acc, cg8* p, uint64_t nstripes)
+{
+	const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+	cg32* q = reinterpret_cast<cg32*>(a & ~uintptr_t(3));
+	const uint32_t sh = uint32_t(a & 3u);
+	return sh ? xxh32_stripes_impl<true>(acc, q, sh, nstripes)
+	          : xxh32_stripes_impl<false>(acc, q, 0, nstripes);
 }
 
 // XXHash32.Final (lz4ada.adb:993-1017) from the 4 lanes + tail buffer.
@@ -131,7 +199,7 @@ __device__ uint32_t xxh32_final_dev(uint32_t v0, uint32_t v1, uint32_t v2, uint3
 }
 
 // One-shot XXH32 (seed 0) of [p, p+n) by a whole wave (XXHash32.Hash).
-__device__ uint32_t wave_xxh32(const uint8_t* p, uint64_t n)
+__device__ uint32_t wave_xxh32(cg8* p, uint64_t n)
 {
 	const uint32_t lane = lane_id();
 	const uint32_t init[4] = { P1 + P2, P2, 0u, 0u - P1 };
@@ -158,7 +226,7 @@ __global__ __launch_bounds__(64) void k_block_checksums(const uint8_t* __restric
 	const lz4ada_block_desc d = desc[b];
 	if (!(d.flags & LZ4ADA_BLOCK_HAS_CKSUM))
 		return;
-	uint32_t h = wave_xxh32(frame + d.in_off, d.in_len);
+	uint32_t h = wave_xxh32(gptr(frame) + d.in_off, d.in_len);
 	if (lane_id() == 0)
 		st[b].cksum = h;
 }
@@ -172,7 +240,7 @@ __global__ __launch_bounds__(64) void k_output_checksums(const uint8_t* __restri
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
 		return;
-	uint32_t h = wave_xxh32(out + desc[b].out_off, st[b].out_len);
+	uint32_t h = wave_xxh32(gptr(out) + desc[b].out_off, st[b].out_len);
 	if (lane_id() == 0)
 		hash[b] = h;
 }
@@ -190,10 +258,11 @@ __global__ __launch_bounds__(64) void k_xxh32_update(lz4ada_xxh32_state* __restr
 		buf[i] = s->buffer[i];
 	uint64_t total = s->total_length + len;
 	uint64_t pos = 0;
+	cg8* dg = gptr(data);
 	// Refill a partially filled stripe byte by byte (Update1, :965-977).
 	if (bs > 0) {
 		while (bs < 16 && pos < len)
-			buf[bs++] = data[pos++];
+			buf[bs++] = dg[pos++];
 		if (bs == 16) {
 			uint32_t w = uint32_t(buf[4 * (lane & 3u)]) |
 			             (uint32_t(buf[4 * (lane & 3u) + 1]) << 8) |
@@ -205,10 +274,10 @@ __global__ __launch_bounds__(64) void k_xxh32_update(lz4ada_xxh32_state* __restr
 	}
 	if (bs == 0) {
 		const uint64_t ns = (len - pos) / 16;
-		acc = wave_xxh32_stripes(acc, data + pos, ns);
+		acc = wave_xxh32_stripes(acc, dg + pos, ns);
 		pos += ns * 16;
 		while (pos < len)
-			buf[bs++] = data[pos++];
+			buf[bs++] = dg[pos++];
 	}
 	uint32_t v0 = __shfl(acc, 0), v1 = __shfl(acc, 1), v2 = __shfl(acc, 2), v3 = __shfl(acc, 3);
 	uint32_t h = xxh32_final_dev(v0, v1, v2, v3, buf, bs, total);
@@ -227,82 +296,17 @@ __global__ __launch_bounds__(64) void k_xxh32_update(lz4ada_xxh32_state* __restr
 
 // --------------------------------------------------------- block decoder
 
-constexpr int WIN = 1024;        // LDS window of compressed bytes
-constexpr int NC = 256;          // speculative token candidates per step
-constexpr int TERM = 0xffff;     // jump-table terminal
-constexpr int LOOKAHEAD = 544;   // bytes a candidate token may touch
-constexpr int OUTB = 4096;       // LDS batch output capacity
-constexpr int BIG = 256;         // longer sequences take the one-token path
+constexpr int INB = 4096;        // compressed staging ring per wave (LDS)
+constexpr int INB_MASK = INB - 1;
+constexpr int LOOK = 352;        // bytes past a 64-byte window a token may touch
+constexpr int OUTB = 2048;       // batch output bytes (32 chunks of 64)
+constexpr int MAXTOK = 64;       // tokens per batch (one per lane)
+constexpr int WTOK = 32;         // tokens taken from one 64-byte window (<= 21 fit)
+constexpr int BIG = 512;         // longer sequences take the one-token path
+constexpr int SPAN = 2048;       // compressed bytes a batch may span
+constexpr int32_t TERM = 1 << 30;
 
 enum TokKind : int { TK_NORMAL = 0, TK_LAST = 1, TK_COMPLEX = 2, TK_ERR = 3 };
-
-struct Tok {
-	int32_t lit;   // block-relative literal start
-	int32_t L;     // literal count
-	int32_t ml;    // match length incl. +4 (0 for TK_LAST)
-	int32_t off;   // match offset
-	int32_t next;  // block-relative position of the next token
-	int32_t kind;
-};
-
-// Parse the token at block-relative position c from the LDS window.
-// wofs maps block-relative x to window index x + wofs; wend is the
-// block-relative end of the window.  Only single-byte length extensions
-// are resolved here (TK_COMPLEX otherwise).  Mirrors Decompress_Sequence
-// (lz4ada.adb:737-777) for the non-error cases; every malformed shape is
-// TK_ERR and left to the one-token path, which raises precisely.
-__device__ __forceinline__ Tok parse_tok(const uint8_t* win, int64_t wofs, int64_t c,
-                                         int64_t n, int64_t wend)
-{
-	Tok t;
-	t.lit = 0;
-	t.L = 0;
-	t.ml = 0;
-	t.off = 0;
-	t.next = 0;
-	t.kind = TK_ERR;
-	if (c >= n || c >= wend)
-		return t;
-	const uint32_t tk = win[c + wofs];
-	int64_t L = tk >> 4, M = tk & 15, p = c + 1;
-	if (L == 15) {
-		if (p >= n) return t;
-		if (p >= wend) { t.kind = TK_COMPLEX; return t; }
-		uint32_t e = win[p + wofs];
-		++p;
-		if (e == 255) { t.kind = TK_COMPLEX; return t; }
-		L += e;
-	}
-	t.lit = int32_t(p);
-	t.L = int32_t(L);
-	p += L;
-	if (p > wend) { t.kind = TK_COMPLEX; return t; }
-	if (p >= n) {
-		if (p == n && M == 0) {
-			t.kind = TK_LAST;
-			t.next = int32_t(n);
-		}
-		return t;  // else ML-after-literals / overrun: TK_ERR
-	}
-	if (p + 1 >= n) return t;
-	if (p + 1 >= wend) { t.kind = TK_COMPLEX; return t; }
-	const uint32_t off = uint32_t(win[p + wofs]) | (uint32_t(win[p + 1 + wofs]) << 8);
-	p += 2;
-	if (off == 0) return t;
-	if (M == 15) {
-		if (p >= n) return t;
-		if (p >= wend) { t.kind = TK_COMPLEX; return t; }
-		uint32_t e = win[p + wofs];
-		++p;
-		if (e == 255) { t.kind = TK_COMPLEX; return t; }
-		M += e;
-	}
-	t.off = int32_t(off);
-	t.ml = int32_t(M + 4);
-	t.next = int32_t(p);
-	t.kind = TK_NORMAL;
-	return t;
-}
 
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v)
 {
@@ -330,7 +334,7 @@ __device__ __forceinline__ int32_t wave_incl_scan(int32_t v)
 // Sum of a length extension (Process_Variable_Length, lz4ada.adb:724-735)
 // starting at block-relative p, 64 bytes per step.  Returns false when the
 // block ends first (D4).  Whole-wave, uniform.
-__device__ bool wave_ext_sum(const uint8_t* in, int64_t n, int64_t& p, int64_t& sum)
+__device__ bool wave_ext_sum(cg8* in, int64_t n, int64_t& p, int64_t& sum)
 {
 	const uint32_t lane = lane_id();
 	for (;;) {
@@ -356,10 +360,9 @@ __device__ bool wave_ext_sum(const uint8_t* in, int64_t n, int64_t& p, int64_t& 
 }
 
 // Wave-cooperative copy of n bytes global -> global (no overlap).
-__device__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t n)
+__device__ void wave_copy(g8* __restrict__ dst, cg8* __restrict__ src, int64_t n)
 {
 	const uint32_t lane = lane_id();
-	// Align the destination to 16 B, then move 16 B per lane per step.
 	int64_t head = int64_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
 	if (head > n)
 		head = n;
@@ -370,22 +373,22 @@ __device__ void wave_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__
 	n -= head;
 	const int64_t nv = n / 16;
 	for (int64_t i = lane; i < nv; i += 64) {
-		const uint8_t* s = src + 16 * i;
-		uint4 v;
-		v.x = ld32u(s);
-		v.y = ld32u(s + 4);
-		v.z = ld32u(s + 8);
-		v.w = ld32u(s + 12);
-		*reinterpret_cast<uint4*>(dst + 16 * i) = v;
+		cg8* sp = src + 16 * i;
+		u32x4 v;
+		v.x = ld32u_cached(sp);
+		v.y = ld32u_cached(sp + 4);
+		v.z = ld32u_cached(sp + 8);
+		v.w = ld32u_cached(sp + 12);
+		*reinterpret_cast<GLOBAL u32x4*>(dst + 16 * i) = v;
 	}
 	for (int64_t i = nv * 16 + lane; i < n; i += 64)
 		dst[i] = src[i];
 }
 
-// One token at block-relative s, wave-cooperative, straight to global
-// memory.  Handles every shape, including the malformed ones.
+// One token at block-relative s, wave-cooperative, global -> global.
+// Handles every shape, including the malformed ones (exact statuses).
 // Returns false with st filled on error; advances s and o.
-__device__ bool one_token(const uint8_t* __restrict__ in, int64_t n, uint8_t* __restrict__ ob,
+__device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
                           int64_t cap, int64_t& s, int64_t& o, lz4ada_block_status& st)
 {
 	const uint32_t lane = lane_id();
@@ -461,13 +464,148 @@ __device__ bool one_token(const uint8_t* __restrict__ in, int64_t n, uint8_t* __
 	} else {
 		// Overlap: byte k repeats source byte (k mod off); every source
 		// byte precedes the match, so all lanes run at once.
-		for (int64_t k = lane; k < ml; k += 64)
-			ob[o + k] = ob[q0 + (k % off)];
+		const uint32_t offu = uint32_t(off);
+		uint32_t k = lane, r = lane % offu;
+		const uint32_t step = 64u % offu;
+		for (; int64_t(k) < ml; k += 64) {
+			ob[o + k] = ob[q0 + r];
+			r += step;
+			if (r >= offu)
+				r -= offu;
+		}
 	}
 	o += ml;
 	s = p;
 	__syncthreads();
 	return true;
+}
+
+// Speculative parse of a token at candidate position c (block-relative)
+// from the LDS staging ring.  Every lane evaluates one position; lanes
+// not on the true chain are discarded later.  Only single-byte length
+// extensions are resolved here (TK_COMPLEX otherwise); every malformed
+// shape is TK_ERR and left to one_token, which reports it exactly
+// (Decompress_Sequence, lz4ada.adb:737-777).
+struct Cand {
+	int32_t L, lit, off, ml, next, kind;
+};
+
+__device__ __forceinline__ Cand parse_cand(const uint8_t* inb, int32_t mis, int32_t c, int32_t n,
+                                           int32_t hi)
+{
+	Cand t;
+	t.L = 0;
+	t.lit = 0;
+	t.off = 0;
+	t.ml = 0;
+	t.next = 0;
+	t.kind = TK_ERR;
+	if (c >= n)
+		return t;
+	const uint32_t tk = inb[(c + mis) & INB_MASK];
+	const uint32_t e1 = inb[(c + 1 + mis) & INB_MASK];
+	int32_t L = int32_t(tk >> 4);
+	const int32_t M = int32_t(tk & 15u);
+	int32_t p = c + 1;
+	if (L == 15) {
+		if (p >= n)
+			return t;
+		if (e1 == 255u) {
+			t.kind = TK_COMPLEX;
+			return t;
+		}
+		L += int32_t(e1);
+		++p;
+	}
+	t.L = L;
+	t.lit = p;
+	p += L;
+	if (p >= n) {
+		if (p == n && M == 0) {
+			t.kind = TK_LAST;
+			t.next = n;
+		}
+		return t;
+	}
+	if (p + 2 > hi) {  // not staged (cannot happen for window tokens)
+		t.kind = TK_COMPLEX;
+		return t;
+	}
+	if (p + 1 >= n)
+		return t;
+	const uint32_t off = uint32_t(inb[(p + mis) & INB_MASK]) | (uint32_t(inb[(p + 1 + mis) & INB_MASK]) << 8);
+	p += 2;
+	if (off == 0)
+		return t;
+	int32_t ml = M + 4;
+	if (M == 15) {
+		if (p >= n)
+			return t;
+		const uint32_t e2 = inb[(p + mis) & INB_MASK];
+		if (e2 == 255u) {
+			t.kind = TK_COMPLEX;
+			return t;
+		}
+		ml += int32_t(e2);
+		++p;
+	}
+	t.off = int32_t(off);
+	t.ml = ml;
+	t.next = p;
+	t.kind = TK_NORMAL;
+	return t;
+}
+
+struct DecLds {
+	uint8_t inb[INB];                // compressed bytes: block-relative x -> inb[(x + mis) & INB_MASK]
+	uint8_t outb[OUTB + 16];         // batch output
+	int32_t fsrc[OUTB];              // per byte: >= 0 pre-batch output pos, < 0 ~compressed pos
+	uint16_t link[OUTB];             // per byte: FINAL, or the in-batch byte it copies
+	int32_t r_tstart[MAXTOK];        // batch tokens: output start (batch-relative)
+	int32_t r_L[MAXTOK];
+	int32_t r_lit[MAXTOK];
+	int32_t r_off[MAXTOK];
+	uint32_t starts[OUTB / 32 + 2];  // bitmap of token starts in the batch output
+};
+
+constexpr uint16_t FINAL = 0xffff;
+
+// Cross-lane hand-off through LDS inside one wavefront: LDS executes a
+// wave's operations in order, so only the compiler must not reorder.
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
+
+// Stage compressed bytes so that block-relative [lo, need) is in the ring.
+// Block-relative x lives at inb[(x + mis) & INB_MASK], mis = in & 15, so the
+// 16-byte global chunks land 16-byte aligned.  `hi` is block-relative.
+__device__ __forceinline__ void stage_to(DecLds& L, cg8* in, uintptr_t lim_addr,
+                                         int32_t mis, int32_t& hi, int32_t lo, int32_t need)
+{
+	const uint32_t lane = lane_id();
+	const uintptr_t in_addr = reinterpret_cast<uintptr_t>(in);
+	if (hi < lo)  // skipped ahead (one-token path): restart at lo
+		hi = ((lo + mis) & ~15) - mis;
+	bool any = false;
+	while (hi < need) {
+		const uintptr_t ga = in_addr + uintptr_t(intptr_t(hi)) + 16u * lane;  // 16-aligned
+		u32x4 v;
+		if (ga + 16 <= lim_addr) {
+			v = *reinterpret_cast<const GLOBAL u32x4*>(ga);
+		} else {
+			uint8_t t[16];
+			for (int i = 0; i < 16; ++i)
+				t[i] = (ga + i < lim_addr) ? *reinterpret_cast<cg8*>(ga + i) : 0;
+			v.x = t[0] | (t[1] << 8) | (t[2] << 16) | (uint32_t(t[3]) << 24);
+			v.y = t[4] | (t[5] << 8) | (t[6] << 16) | (uint32_t(t[7]) << 24);
+			v.z = t[8] | (t[9] << 8) | (t[10] << 16) | (uint32_t(t[11]) << 24);
+			v.w = t[12] | (t[13] << 8) | (t[14] << 16) | (uint32_t(t[15]) << 24);
+		}
+		const uint32_t idx = uint32_t(hi + mis + 16 * int32_t(lane)) & INB_MASK;
+		*reinterpret_cast<u32x4*>(&L.inb[idx]) = v;
+		hi += 1024;
+		any = true;
+	}
+	if (any)
+		wave_lds_fence();
 }
 
 __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict__ frame,
@@ -476,19 +614,17 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
                                                        uint32_t nblocks, uint8_t* __restrict__ out,
                                                        lz4ada_block_status* __restrict__ status)
 {
-	__shared__ __attribute__((aligned(16))) uint8_t win[WIN];
-	__shared__ uint16_t J[6][NC];
-	__shared__ __attribute__((aligned(16))) uint8_t outb[OUTB];
+	__shared__ DecLds L;
 
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
 		return;
-	const uint32_t lane = lane_id();
+	const int lane = int(lane_id());
 	const lz4ada_block_desc d = desc[b];
-	const uint8_t* __restrict__ in = frame + d.in_off;
-	uint8_t* __restrict__ ob = out + d.out_off;
-	const int64_t n = d.in_len;
-	const int64_t cap = d.out_cap;
+	cg8* __restrict__ in = gptr(frame) + d.in_off;
+	g8* __restrict__ ob = gptr(out) + d.out_off;
+	const int32_t n = int32_t(d.in_len);
+	const int32_t cap = int32_t(d.out_cap);
 
 	lz4ada_block_status st;
 	st.code = DS_OK;
@@ -514,132 +650,229 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 		return;
 	}
 
-	const uintptr_t in_addr = reinterpret_cast<uintptr_t>(in);
 	const uintptr_t lim_addr = reinterpret_cast<uintptr_t>(frame) + frame_len;
-	int64_t s = 0, o = 0;
-	int64_t wofs = 0, wend = -1;  // window: block-relative [wend - WIN, wend)
+	int32_t s = 0;       // block-relative compressed position of the chain
+	int32_t o = 0;       // block-relative output position (flushed)
+	int32_t hi = 0;      // staged compressed bytes end (block-relative)
+	int32_t nb = 0;      // tokens in the current batch
+	int32_t blen = 0;    // batch output bytes
+	int32_t bcomp0 = 0;  // compressed position of the batch's first token
 	bool ok = true;
+	bool done = (n == 0);
+	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+	hi = -mis;  // staging is chunked on 16-byte aligned global addresses
 
-	while (s < n) {
-		// ---- (re)stage the compressed window so [s, s + LOOKAHEAD) is in it
-		if (s + LOOKAHEAD > wend || s + wofs < 0) {
-			const uintptr_t wg = (in_addr + uintptr_t(s)) & ~uintptr_t(15);
-			const uintptr_t ga = wg + 16u * lane;
-			uint4 v;
-			if (ga + 16 <= lim_addr) {
-				v = *reinterpret_cast<const uint4*>(ga);
+	for (int32_t iter = 0; !done; ++iter) {
+		if (iter > 4 * n + 64) {  // every iteration makes progress; never spin
+			st.code = DS_INTERNAL;
+			ok = false;
+			break;
+		}
+		// ------------------------------------------------ window parse at s
+		bool stop = false;       // next token needs the one-token path
+		bool end_block = false;  // chain reached the block end
+		bool force_flush = false;
+		{
+			stage_to(L, in, lim_addr, mis, hi, nb ? bcomp0 : s, s + 64 + LOOK);
+			const int32_t c = s + lane;
+			const Cand t = parse_cand(L.inb, mis, c, n, hi);
+			int32_t f = (t.kind == TK_NORMAL) ? t.next : (TERM | c);
+			int32_t fr[5];
+#pragma unroll
+			for (int r = 0; r < 5; ++r) {
+				fr[r] = f;
+				const bool inw = !(f & TERM) && f < s + 64;
+				const int32_t g = __shfl(f, inw ? f - s : lane);
+				f = inw ? g : f;
+			}
+			// lane j: position of the j-th token of the chain from s
+			int32_t cj = s;
+#pragma unroll
+			for (int r = 0; r < 5; ++r) {
+				const bool inw = !(cj & TERM) && cj < s + 64;
+				const int32_t g = __shfl(fr[r], inw ? cj - s : 0);
+				if ((lane >> r) & 1)
+					cj = inw ? g : cj;
+			}
+			const bool inwin = !(cj & TERM) && cj < s + 64 && lane < WTOK;
+			const int src = inwin ? cj - s : 0;
+			const int32_t kL = __shfl(t.L, src), klit = __shfl(t.lit, src);
+			const int32_t koff = __shfl(t.off, src), kml = __shfl(t.ml, src);
+			const int32_t knext = __shfl(t.next, src), kkind = __shfl(t.kind, src);
+			const bool good = inwin && (kkind == TK_NORMAL || kkind == TK_LAST);
+			const int32_t klen = kL + (kkind == TK_NORMAL ? kml : 0);
+			// cut: capacity, long tokens, pre-block references, D5
+			const int32_t room_tok = MAXTOK - nb;
+			const int32_t incl = wave_incl_scan(good ? klen : 0);
+			const int32_t tstart = blen + incl - klen;
+			const int32_t d0 = o + tstart + kL;  // block-relative match start
+			const bool fits = good && lane < room_tok && klen <= BIG && blen + incl <= OUTB &&
+			                  o + blen + incl <= cap && (kkind != TK_NORMAL || d0 - koff >= 0);
+			const uint64_t badm = __ballot(!fits);
+			const int cnt = badm ? (__ffsll((long long)badm) - 1) : 64;
+			// what comes after the taken tokens
+			const int32_t cnext = cnt > 0 ? __shfl(knext, cnt - 1) : s;
+			const int32_t ckind_last = cnt > 0 ? __shfl(kkind, cnt - 1) : TK_NORMAL;
+			if (lane < cnt) {
+				L.r_tstart[nb + lane] = tstart;
+				L.r_L[nb + lane] = kL;
+				L.r_lit[nb + lane] = klit;
+				L.r_off[nb + lane] = koff;
+			}
+			const bool was_empty = (nb == 0);
+			if (was_empty && cnt > 0)
+				bcomp0 = s;
+			const int32_t add = cnt > 0 ? __shfl(incl, cnt - 1) : 0;
+			nb += cnt;
+			blen += add;
+			if (cnt > 0 && ckind_last == TK_LAST) {
+				end_block = true;
+				s = n;
+			} else if (cnt > 0 && cnext >= n) {
+				end_block = true;  // block ends right after a match (lz4ada.adb:780)
+				s = cnext;
+			} else if (cnt > 0) {
+				s = cnext;  // the chain continues; the next window starts there
+			} else if (was_empty) {
+				stop = true;  // the token at s needs the one-token path
 			} else {
-				uint8_t t[16];
-				for (int i = 0; i < 16; ++i)
-					t[i] = (ga + i < lim_addr) ? *reinterpret_cast<const uint8_t*>(ga + i) : 0;
-				v.x = t[0] | (t[1] << 8) | (t[2] << 16) | (uint32_t(t[3]) << 24);
-				v.y = t[4] | (t[5] << 8) | (t[6] << 16) | (uint32_t(t[7]) << 24);
-				v.z = t[8] | (t[9] << 8) | (t[10] << 16) | (uint32_t(t[11]) << 24);
-				v.w = t[12] | (t[13] << 8) | (t[14] << 16) | (uint32_t(t[15]) << 24);
+				force_flush = true;  // batch full: flush, then retry at s
 			}
-			*reinterpret_cast<uint4*>(&win[16 * lane]) = v;
-			wofs = int64_t(in_addr - wg);
-			wend = WIN - wofs;
-			__syncthreads();
 		}
-
-		// ---- speculative candidates: next-token pointer for s + [0, 256)
-#pragma unroll
-		for (int i = 0; i < NC / 64; ++i) {
-			const int k = int(lane) + 64 * i;
-			const Tok t = parse_tok(win, wofs, s + k, n, wend);
-			int nx = TERM;
-			if (t.kind == TK_NORMAL) {
-				const int64_t rel = int64_t(t.next) - s;
-				if (rel < NC)
-					nx = int(rel);
+		wave_lds_fence();
+		const bool flush = end_block || stop || force_flush || nb >= MAXTOK - 8 ||
+		                   blen > OUTB - BIG || (s - bcomp0) >= SPAN;
+		if (flush && nb > 0) {
+			// ------------------------------------------- batch resolve
+			// token k lives in lane k
+			const bool tl = lane < nb;
+			const int32_t k_ts = tl ? L.r_tstart[lane] : 0x7fffffff;
+			const int32_t k_L = tl ? L.r_L[lane] : 0;
+			const int32_t k_lit = tl ? L.r_lit[lane] : 0;
+			const int32_t k_off = tl ? L.r_off[lane] : 1;
+			for (int w = lane; w < OUTB / 32 + 2; w += 64)
+				L.starts[w] = 0u;
+			wave_lds_fence();
+			if (tl)
+				atomicOr(&L.starts[k_ts >> 5], 1u << (k_ts & 31));
+			wave_lds_fence();
+			// pass 1: each byte -> literal (compressed pos), pre-batch output
+			// pos (final after pass 2), or the earlier in-batch byte it copies
+			int32_t kbase = -1;
+			uint32_t pending = 0;  // chunks holding in-batch copies
+#pragma unroll 1
+			for (int32_t X = 0; X < blen; X += 64) {
+				const uint64_t m = uint64_t(L.starts[X >> 5]) |
+				                   (uint64_t(L.starts[(X >> 5) + 1]) << 32);
+				const uint64_t upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+				int32_t k = kbase + __popcll(m & upto);
+				kbase += __popcll(m);
+				k = k < 0 ? 0 : (k >= nb ? nb - 1 : k);
+				const int32_t ts = __shfl(k_ts, k), tL = __shfl(k_L, k);
+				const int32_t tlit = __shfl(k_lit, k), toff = __shfl(k_off, k);
+				const int32_t x = X + lane;
+				bool inb_copy = false;
+				if (x < blen) {
+					int32_t fs = 0;
+					uint16_t ln = FINAL;
+					if (x < ts + tL) {
+						fs = ~(tlit + (x - ts));
+					} else {
+						const int32_t j = x - (ts + tL);
+						const int32_t srcp = o + ts + tL - toff + (j < toff ? j : j % toff);
+						if (srcp < o) {
+							fs = srcp;
+						} else {
+							ln = uint16_t(srcp - o);
+							inb_copy = true;
+						}
+					}
+					L.fsrc[x] = fs;
+					L.link[x] = ln;
+				}
+				if (__ballot(inb_copy))
+					pending |= 1u << (X >> 6);
 			}
-			J[0][k] = uint16_t(nx);
-		}
-		__syncthreads();
-		// ---- pointer doubling: J[r+1][k] = J[r][J[r][k]]
+			wave_lds_fence();
+			// pass 2: fetch every final byte; 8 chunks of loads in flight
+#pragma unroll 1
+			for (int32_t X = 0; X < blen; X += 512) {
+				int32_t fv[8];
+				uint32_t gv[8], lv[8];
 #pragma unroll
-		for (int r = 0; r < 5; ++r) {
+				for (int u = 0; u < 8; ++u) {
+					const int32_t x = X + 64 * u + lane;
+					fv[u] = (x < blen) ? L.fsrc[x] : 0;
+				}
 #pragma unroll
-			for (int i = 0; i < NC / 64; ++i) {
-				const int k = int(lane) + 64 * i;
-				const int a = J[r][k];
-				J[r + 1][k] = uint16_t(a == TERM ? TERM : J[r][a]);
-			}
-			__syncthreads();
-		}
-		// ---- lane j finds the j-th token of the chain that starts at s
-		int c = 0;
+				for (int u = 0; u < 8; ++u)
+					gv[u] = ob[fv[u] >= 0 ? fv[u] : 0];
 #pragma unroll
-		for (int r = 0; r < 6; ++r) {
-			if (((lane >> r) & 1u) && c != TERM)
-				c = J[r][c];
-		}
-		const bool inchain = (c != TERM);
-		Tok t = parse_tok(win, wofs, s + (inchain ? c : 0), n, wend);
-		const int32_t len = (t.kind == TK_NORMAL) ? t.L + t.ml : (t.kind == TK_LAST ? t.L : 0);
-		bool good = inchain && (t.kind == TK_NORMAL || t.kind == TK_LAST) && len <= BIG;
-		// batch = longest prefix of good lanes that fits OUTB, the block
-		// slot, and references nothing before the block start
-		const uint64_t bad0 = __ballot(!good);
-		int cnt = bad0 ? (__ffsll((long long)bad0) - 1) : 64;
-		const int32_t lenm = (int(lane) < cnt) ? len : 0;
-		const int32_t incl = wave_incl_scan(lenm);
-		const int32_t ostart = incl - lenm;
-		const int64_t d0 = o + ostart + t.L;           // match destination
-		const int64_t q0 = d0 - t.off;                  // match source start
-		const bool fits = (incl <= OUTB) && (o + incl <= cap) &&
-		                  (t.kind != TK_NORMAL || q0 >= 0);
-		const uint64_t bad1 = __ballot(!(fits) && int(lane) < cnt);
-		if (bad1) {
-			const int f = __ffsll((long long)bad1) - 1;
-			cnt = f < cnt ? f : cnt;
-		}
-		if (cnt == 0) {
-			__syncthreads();
-			if (!one_token(in, n, ob, cap, s, o, st)) {
-				ok = false;
-				break;
-			}
-			continue;
-		}
-		const bool mine = int(lane) < cnt;
-		const int32_t blen = __shfl(incl, cnt - 1);
-		const int32_t last_next = __shfl(t.next, cnt - 1);
-
-		// ---- literals: window -> batch buffer
-		if (mine) {
-			const int64_t src = t.lit + wofs;
-			for (int32_t i = 0; i < t.L; ++i)
-				outb[ostart + i] = win[src + i];
-		}
-		__syncthreads();
-		// ---- matches, in dependency rounds
-		bool pend = mine && t.kind == TK_NORMAL;
-		const int64_t srcend = (q0 + t.ml < d0) ? q0 + t.ml : d0;
-		while (__ballot(pend)) {
-			const int64_t m = wave_min_i64(pend ? d0 : INT64_MAX);
-			const bool ready = pend && srcend <= m;
-			if (ready) {
-				const int32_t ml = t.ml, off = t.off;
-				int32_t r = 0;
-				for (int32_t k = 0; k < ml; ++k) {
-					const int64_t sp = q0 + r;
-					const uint8_t v = (sp < o) ? ob[sp] : outb[sp - o];
-					outb[d0 - o + k] = v;
-					if (++r == off)
-						r = 0;
+				for (int u = 0; u < 8; ++u)
+					lv[u] = L.inb[((fv[u] < 0 ? ~fv[u] : 0) + mis) & INB_MASK];
+#pragma unroll
+				for (int u = 0; u < 8; ++u) {
+					const int32_t x = X + 64 * u + lane;
+					if (x < blen && L.link[x] == FINAL)
+						L.outb[x] = uint8_t(fv[u] >= 0 ? gv[u] : lv[u]);
 				}
 			}
-			pend = pend && !ready;
+			wave_lds_fence();
+			// pass 3: in-batch copies read the final byte at the end of
+			// their link chain (every link points strictly backwards)
+			while (pending) {
+				const int ch = __ffs(pending) - 1;
+				pending &= pending - 1;
+				const int32_t x = ch * 64 + lane;
+				if (x < blen) {
+					uint32_t y = L.link[x];
+					if (y != FINAL) {
+						for (int guard = 0; guard <= OUTB; ++guard) {
+							const uint32_t z = L.link[y];
+							if (z == FINAL)
+								break;
+							y = z;
+						}
+						L.outb[x] = L.outb[y];
+					}
+				}
+			}
 			__syncthreads();
+			// flush the batch to HBM
+			{
+				g8* dst = ob + o;
+				const int32_t head = int32_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
+				const int32_t h = head < blen ? head : blen;
+				if (lane < h)
+					dst[lane] = L.outb[lane];
+				const int32_t nv = (blen - h) / 16;
+				for (int32_t i = lane; i < nv; i += 64) {
+					u32x4 v;
+					__builtin_memcpy(&v, &L.outb[h + 16 * i], 16);
+					*reinterpret_cast<GLOBAL u32x4*>(dst + h + 16 * i) = v;
+				}
+				for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)
+					dst[i] = L.outb[i];
+			}
+			__syncthreads();
+			o += blen;
+			nb = 0;
+			blen = 0;
 		}
-		// ---- flush the batch to HBM
-		for (int32_t i = int32_t(lane); i < blen; i += 64)
-			ob[o + i] = outb[i];
-		__syncthreads();
-		o += blen;
-		s = last_next;
+		if (end_block) {
+			done = true;
+		} else if (stop) {
+			int64_t s64 = s, o64 = o;
+			if (!one_token(in, n, ob, cap, s64, o64, st)) {
+				ok = false;
+				done = true;
+			} else {
+				s = int32_t(s64);
+				o = int32_t(o64);
+				if (s >= n)
+					done = true;
+			}
+		}
 	}
 
 	if (lane == 0) {
