@@ -296,17 +296,46 @@ __global__ __launch_bounds__(64) void k_xxh32_update(lz4ada_xxh32_state* __restr
 
 // --------------------------------------------------------- block decoder
 
-constexpr int INB = 4096;        // compressed staging ring per wave (LDS)
+constexpr int INB = 8192;        // compressed staging ring per wave (LDS)
 constexpr int INB_MASK = INB - 1;
-constexpr int LOOK = 352;        // bytes past a 64-byte window a token may touch
-constexpr int OUTB = 2048;       // batch output bytes (32 chunks of 64)
+constexpr int WIN = 256;         // speculative parse window (4 candidates per lane)
+constexpr int LOOK = WIN + 288;  // bytes past s a window's tokens may touch
+constexpr int OUTB = 4096;       // batch output bytes
 constexpr int MAXTOK = 64;       // tokens per batch (one per lane)
-constexpr int WTOK = 32;         // tokens taken from one 64-byte window (<= 21 fit)
-constexpr int BIG = 512;         // longer sequences take the one-token path
+constexpr int WTOK = 64;         // tokens taken from one window (one per lane)
+constexpr int BIG = 1024;        // longer sequences take the one-token path
 constexpr int SPAN = 2048;       // compressed bytes a batch may span
-constexpr int32_t TERM = 1 << 30;
 
 enum TokKind : int { TK_NORMAL = 0, TK_LAST = 1, TK_COMPLEX = 2, TK_ERR = 3 };
+
+// Diagnostic build only (make stamps -> liblz4ada_hip_stamps.so): per-phase
+// s_memtime sums of k_decode_blocks, read back by tools/stamps.py.  The
+// product library is built without LZ4ADA_STAMPS and executes no stamp.
+enum StampPhase { SP_STAGE, SP_CAND, SP_DOUBLE, SP_SELECT, SP_LIT, SP_MATCH, SP_FLUSH, SP_ONE,
+	          SP_BATCHES, SP_WINDOWS, SP_TOKENS, SP_ROUNDS, SP_N };
+#ifdef LZ4ADA_STAMPS
+__device__ unsigned long long g_stamps[SP_N];
+#define STAMP_DECL uint64_t st_acc[SP_N] = {}; uint64_t st_t = __builtin_amdgcn_s_memtime()
+#define STAMP(ph)                                                                  \
+	do {                                                                       \
+		asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");        \
+		const uint64_t _t = __builtin_amdgcn_s_memtime();                  \
+		st_acc[ph] += _t - st_t;                                           \
+		st_t = _t;                                                         \
+	} while (0)
+#define STAMP_COUNT(ph, v) (st_acc[ph] += uint64_t(v))
+#define STAMP_FLUSH()                                                              \
+	do {                                                                       \
+		if (lane_id() == 0)                                                \
+			for (int _i = 0; _i < SP_N; ++_i)                          \
+				atomicAdd(&g_stamps[_i], (unsigned long long)st_acc[_i]); \
+	} while (0)
+#else
+#define STAMP_DECL
+#define STAMP(ph)
+#define STAMP_COUNT(ph, v)
+#define STAMP_FLUSH()
+#endif
 
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v)
 {
@@ -318,16 +347,16 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v)
 	return v;
 }
 
-// Inclusive prefix sum over the wave.
+// Inclusive prefix sum over the wave with DPP (row_shr within 16-lane rows,
+// then row_bcast:15 / row_bcast:31 across rows) -- VALU latency, no LDS.
 __device__ __forceinline__ int32_t wave_incl_scan(int32_t v)
 {
-	const int lane = int(lane_id());
-#pragma unroll
-	for (int d = 1; d < 64; d <<= 1) {
-		int32_t o = __shfl_up(v, d);
-		if (lane >= d)
-			v += o;
-	}
+	v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+	v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+	v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+	v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+	v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+	v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
 	return v;
 }
 
@@ -480,132 +509,254 @@ __device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
 	return true;
 }
 
-// Speculative parse of a token at candidate position c (block-relative)
-// from the LDS staging ring.  Every lane evaluates one position; lanes
-// not on the true chain are discarded later.  Only single-byte length
-// extensions are resolved here (TK_COMPLEX otherwise); every malformed
-// shape is TK_ERR and left to one_token, which reports it exactly
-// (Decompress_Sequence, lz4ada.adb:737-777).
+// ---------------------------------------------------------- V3 decoder
+//
+// One wavefront per block.  State: s = block-relative compressed position
+// of the token chain, o = block-relative output already flushed to HBM.
+//
+//  1. stage: compressed bytes live in an LDS ring (16-byte global chunks,
+//     1 KiB per refill, the next refill already in flight in registers).
+//  2. parse window [s, s+64): every lane evaluates a token at s + lane
+//     (branch-free, two LDS reads), ds_bpermute pointer doubling finds the
+//     chain from s, lane j picks up the j-th token.  Tokens accumulate into
+//     a batch of up to 64 (one per lane) in LDS records.
+//  3. copy the batch into an LDS output buffer, lane per token, 16 bytes
+//     per step: literals from the ring, matches from HBM (pre-batch) or the
+//     buffer (in-batch, in dependency rounds), then flush with 16-byte
+//     stores.
+//  4. anything unusual -> one_token (wave-cooperative, exact statuses).
+
+constexpr int MIRROR = 16;
+
 struct Cand {
 	int32_t L, lit, off, ml, next, kind;
 };
 
-__device__ __forceinline__ Cand parse_cand(const uint8_t* inb, int32_t mis, int32_t c, int32_t n,
-                                           int32_t hi)
+__device__ __forceinline__ uint32_t lds_u16(const uint8_t* p)
 {
+	uint16_t v;
+	__builtin_memcpy(&v, p, 2);
+	return v;
+}
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t* p)
+{
+	uint32_t v;
+	__builtin_memcpy(&v, p, 4);
+	return v;
+}
+
+// Branch-free token parse at block-relative c from the staging ring
+// (Decompress_Sequence, lz4ada.adb:737-777).  Only single-byte length
+// extensions are resolved here; longer ones are TK_COMPLEX, malformed
+// shapes TK_ERR -- both go to one_token, which reports them exactly.
+__device__ __forceinline__ Cand parse_cand(const uint8_t* inb, int32_t mis, int32_t c, int32_t n)
+{
+	const uint32_t t2 = lds_u16(inb + ((c + mis) & INB_MASK));
+	const int32_t tk = int32_t(t2 & 0xffu), e1 = int32_t(t2 >> 8);
+	const int32_t L0 = tk >> 4, M0 = tk & 15;
+	const bool x1 = (L0 == 15), x2 = (M0 == 15);
+	const int32_t L = L0 + (x1 ? e1 : 0);
+	const int32_t lit = c + 1 + (x1 ? 1 : 0);
+	const int32_t p = lit + L;  // offset position
+	const uint32_t w = lds_u32(inb + ((p + mis) & INB_MASK));
+	const int32_t off = int32_t(w & 0xffffu), e2 = int32_t((w >> 16) & 0xffu);
+	const int32_t ml = M0 + 4 + (x2 ? e2 : 0);
+	const int32_t next = p + 2 + (x2 ? 1 : 0);
+	const bool last = (p == n) && (M0 == 0);
+	const bool err = (c >= n) || (x1 && c + 1 >= n) || (p > n) || (p == n && M0 != 0) ||
+	                 (p < n && (p + 1 >= n || off == 0 || (x2 && p + 2 >= n)));
+	const bool cx = (x1 && e1 == 255) || (x2 && e2 == 255);
 	Cand t;
-	t.L = 0;
-	t.lit = 0;
-	t.off = 0;
-	t.ml = 0;
-	t.next = 0;
-	t.kind = TK_ERR;
-	if (c >= n)
-		return t;
-	const uint32_t tk = inb[(c + mis) & INB_MASK];
-	const uint32_t e1 = inb[(c + 1 + mis) & INB_MASK];
-	int32_t L = int32_t(tk >> 4);
-	const int32_t M = int32_t(tk & 15u);
-	int32_t p = c + 1;
-	if (L == 15) {
-		if (p >= n)
-			return t;
-		if (e1 == 255u) {
-			t.kind = TK_COMPLEX;
-			return t;
-		}
-		L += int32_t(e1);
-		++p;
-	}
 	t.L = L;
-	t.lit = p;
-	p += L;
-	if (p >= n) {
-		if (p == n && M == 0) {
-			t.kind = TK_LAST;
-			t.next = n;
-		}
-		return t;
-	}
-	if (p + 2 > hi) {  // not staged (cannot happen for window tokens)
-		t.kind = TK_COMPLEX;
-		return t;
-	}
-	if (p + 1 >= n)
-		return t;
-	const uint32_t off = uint32_t(inb[(p + mis) & INB_MASK]) | (uint32_t(inb[(p + 1 + mis) & INB_MASK]) << 8);
-	p += 2;
-	if (off == 0)
-		return t;
-	int32_t ml = M + 4;
-	if (M == 15) {
-		if (p >= n)
-			return t;
-		const uint32_t e2 = inb[(p + mis) & INB_MASK];
-		if (e2 == 255u) {
-			t.kind = TK_COMPLEX;
-			return t;
-		}
-		ml += int32_t(e2);
-		++p;
-	}
-	t.off = int32_t(off);
+	t.lit = lit;
+	t.off = off;
 	t.ml = ml;
-	t.next = p;
-	t.kind = TK_NORMAL;
+	t.next = next;
+	t.kind = err ? TK_ERR : (cx ? TK_COMPLEX : (last ? TK_LAST : TK_NORMAL));
+	if (last) {
+		t.ml = 0;
+		t.off = 0;
+		t.next = n;
+	}
+	if (x1 && e1 == 255)  // L, p and everything after are meaningless
+		t.kind = (c + 1 >= n) ? TK_ERR : TK_COMPLEX;
 	return t;
 }
 
+// Wave-uniform value: every lane holds the same; tell the compiler so it
+// keeps the serial parse in SGPRs with scalar branches.
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Uniform (scalar) parse of the token at s from the staging ring, with
+// length extensions of any size, for tokens the speculative window cannot
+// take (long literal runs).  Returns false when the token is malformed or
+// not fully staged; one_token then handles it.
+__device__ __forceinline__ bool parse_serial(const uint8_t* inb, int32_t mis, int32_t s, int32_t n,
+                                             int32_t hi, Cand& t)
+{
+	s = uni(s);
+	n = uni(n);
+	hi = uni(hi);
+	mis = uni(mis);
+	if (s >= n || s + 2 > hi)
+		return false;
+	const int32_t tk = uni(inb[(s + mis) & INB_MASK]);
+	int32_t L = tk >> 4, M = tk & 15, p = s + 1;
+	bool ok = true;
+	if (L == 15) {
+		int32_t e = 255;
+		while (ok && e == 255) {
+			if (p >= n || p >= hi) {
+				ok = false;
+			} else {
+				e = uni(inb[(p + mis) & INB_MASK]);
+				++p;
+				L += e;
+			}
+		}
+	}
+	const int32_t lit = p;
+	p += L;
+	int32_t off = 0, ml = 0, next = n, kind = TK_ERR;
+	if (ok) {
+		if (p >= n) {
+			if (p == n && M == 0 && p <= hi)
+				kind = TK_LAST;
+		} else if (p + 3 <= hi && p + 1 < n) {
+			off = uni(inb[(p + mis) & INB_MASK]) | (uni(inb[(p + 1 + mis) & INB_MASK]) << 8);
+			p += 2;
+			if (off != 0) {
+				bool okm = true;
+				if (M == 15) {
+					int32_t e = 255;
+					while (okm && e == 255) {
+						if (p >= n || p >= hi) {
+							okm = false;
+						} else {
+							e = uni(inb[(p + mis) & INB_MASK]);
+							++p;
+							M += e;
+						}
+					}
+				}
+				if (okm) {
+					ml = M + 4;
+					next = p;
+					kind = TK_NORMAL;
+				}
+			}
+		}
+	}
+	t.lit = lit;
+	t.L = L;
+	t.off = kind == TK_NORMAL ? off : 0;
+	t.ml = kind == TK_NORMAL ? ml : 0;
+	t.next = next;
+	t.kind = kind;
+	return kind == TK_NORMAL || kind == TK_LAST;
+}
+
+// Index of the last batch token whose output starts at or before x
+// (tokens live one per lane, ts ascending).
+__device__ __forceinline__ int32_t owner_of(int32_t ts_reg, int32_t nb, int32_t x)
+{
+	int32_t lo = 0, hi = nb - 1;
+#pragma unroll
+	for (int i = 0; i < 6; ++i) {
+		const int32_t mid = (lo + hi + 1) >> 1;
+		const int32_t t = __shfl(ts_reg, mid);
+		if (t <= x)
+			lo = mid;
+		else
+			hi = mid - 1;
+	}
+	return lo;
+}
+
 struct DecLds {
-	uint8_t inb[INB];                // compressed bytes: block-relative x -> inb[(x + mis) & INB_MASK]
-	uint8_t outb[OUTB + 16];         // batch output
-	int32_t fsrc[OUTB];              // per byte: >= 0 pre-batch output pos, < 0 ~compressed pos
-	uint16_t link[OUTB];             // per byte: FINAL, or the in-batch byte it copies
-	int32_t r_tstart[MAXTOK];        // batch tokens: output start (batch-relative)
+	uint16_t J[6][WIN];         // J[r][k]: window position 2^r tokens after k (>= WIN: out)
+	uint8_t inb[INB + MIRROR];  // block-relative x -> inb[(x + mis) & INB_MASK]
+	uint8_t outb[OUTB + 32];    // batch output
+	int32_t r_tstart[MAXTOK];   // batch tokens: output start (batch-relative)
 	int32_t r_L[MAXTOK];
 	int32_t r_lit[MAXTOK];
 	int32_t r_off[MAXTOK];
-	uint32_t starts[OUTB / 32 + 2];  // bitmap of token starts in the batch output
+	int32_t r_ml[MAXTOK];
 };
-
-constexpr uint16_t FINAL = 0xffff;
 
 // Cross-lane hand-off through LDS inside one wavefront: LDS executes a
 // wave's operations in order, so only the compiler must not reorder.
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
 
 // Stage compressed bytes so that block-relative [lo, need) is in the ring.
-// Block-relative x lives at inb[(x + mis) & INB_MASK], mis = in & 15, so the
-// 16-byte global chunks land 16-byte aligned.  `hi` is block-relative.
-__device__ __forceinline__ void stage_to(DecLds& L, cg8* in, uintptr_t lim_addr,
-                                         int32_t mis, int32_t& hi, int32_t lo, int32_t need)
+// `pf` holds the 1 KiB chunk at `hi`, loaded ahead; writing it to LDS is
+// the first use, so its load latency overlaps the work since the last call.
+__device__ __forceinline__ u32x4 load_chunk(cg8* in, uintptr_t lim_addr, int32_t at)
 {
 	const uint32_t lane = lane_id();
-	const uintptr_t in_addr = reinterpret_cast<uintptr_t>(in);
-	if (hi < lo)  // skipped ahead (one-token path): restart at lo
+	const uintptr_t ga = reinterpret_cast<uintptr_t>(in) + uintptr_t(intptr_t(at)) + 16u * lane;
+	u32x4 v;
+	if (ga + 16 <= lim_addr) {
+		v = *reinterpret_cast<const GLOBAL u32x4*>(ga);
+	} else {
+		uint8_t t[16];
+		for (int i = 0; i < 16; ++i)
+			t[i] = (ga + i < lim_addr) ? *reinterpret_cast<cg8*>(ga + i) : 0;
+		__builtin_memcpy(&v, t, 16);
+	}
+	return v;
+}
+
+__device__ __forceinline__ void stage_to(DecLds& L, cg8* in, uintptr_t lim_addr, int32_t mis,
+                                         int32_t& hi, u32x4& pf, int32_t lo, int32_t need)
+{
+	const uint32_t lane = lane_id();
+	if (hi < lo) {  // jumped ahead (one-token path): restart the stream at lo
 		hi = ((lo + mis) & ~15) - mis;
+		pf = load_chunk(in, lim_addr, hi);
+	}
 	bool any = false;
 	while (hi < need) {
-		const uintptr_t ga = in_addr + uintptr_t(intptr_t(hi)) + 16u * lane;  // 16-aligned
-		u32x4 v;
-		if (ga + 16 <= lim_addr) {
-			v = *reinterpret_cast<const GLOBAL u32x4*>(ga);
-		} else {
-			uint8_t t[16];
-			for (int i = 0; i < 16; ++i)
-				t[i] = (ga + i < lim_addr) ? *reinterpret_cast<cg8*>(ga + i) : 0;
-			v.x = t[0] | (t[1] << 8) | (t[2] << 16) | (uint32_t(t[3]) << 24);
-			v.y = t[4] | (t[5] << 8) | (t[6] << 16) | (uint32_t(t[7]) << 24);
-			v.z = t[8] | (t[9] << 8) | (t[10] << 16) | (uint32_t(t[11]) << 24);
-			v.w = t[12] | (t[13] << 8) | (t[14] << 16) | (uint32_t(t[15]) << 24);
-		}
 		const uint32_t idx = uint32_t(hi + mis + 16 * int32_t(lane)) & INB_MASK;
-		*reinterpret_cast<u32x4*>(&L.inb[idx]) = v;
+		*reinterpret_cast<u32x4*>(&L.inb[idx]) = pf;
+		if (idx == 0)
+			*reinterpret_cast<u32x4*>(&L.inb[INB]) = pf;  // mirror for wrap-free reads
 		hi += 1024;
+		pf = load_chunk(in, lim_addr, hi);  // next chunk in flight
 		any = true;
 	}
 	if (any)
 		wave_lds_fence();
+}
+
+// Exact-length store of n (0..16) bytes of v to LDS.
+__device__ __forceinline__ void lds_store_n(uint8_t* dst, u32x4 v, int32_t n)
+{
+	if (n >= 16) {
+		__builtin_memcpy(dst, &v, 16);
+		return;
+	}
+	uint64_t lo = uint64_t(v.x) | (uint64_t(v.y) << 32);
+	uint64_t hi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+	if (n & 8) {
+		__builtin_memcpy(dst, &lo, 8);
+		dst += 8;
+		lo = hi;
+	}
+	if (n & 4) {
+		const uint32_t x = uint32_t(lo);
+		__builtin_memcpy(dst, &x, 4);
+		dst += 4;
+		lo >>= 32;
+	}
+	if (n & 2) {
+		const uint16_t x = uint16_t(lo);
+		__builtin_memcpy(dst, &x, 2);
+		dst += 2;
+		lo >>= 16;
+	}
+	if (n & 1)
+		*dst = uint8_t(lo);
 }
 
 __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict__ frame,
@@ -651,16 +802,17 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 	}
 
 	const uintptr_t lim_addr = reinterpret_cast<uintptr_t>(frame) + frame_len;
+	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
 	int32_t s = 0;       // block-relative compressed position of the chain
 	int32_t o = 0;       // block-relative output position (flushed)
-	int32_t hi = 0;      // staged compressed bytes end (block-relative)
+	int32_t hi = -mis;   // staged compressed bytes end (block-relative)
+	u32x4 pf = load_chunk(in, lim_addr, hi);
 	int32_t nb = 0;      // tokens in the current batch
 	int32_t blen = 0;    // batch output bytes
 	int32_t bcomp0 = 0;  // compressed position of the batch's first token
 	bool ok = true;
 	bool done = (n == 0);
-	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
-	hi = -mis;  // staging is chunked on 16-byte aligned global addresses
+	STAMP_DECL;
 
 	for (int32_t iter = 0; !done; ++iter) {
 		if (iter > 4 * n + 64) {  // every iteration makes progress; never spin
@@ -669,48 +821,109 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 			break;
 		}
 		// ------------------------------------------------ window parse at s
-		bool stop = false;       // next token needs the one-token path
-		bool end_block = false;  // chain reached the block end
-		bool force_flush = false;
+		bool stop = false, end_block = false, force_flush = false;
 		{
-			stage_to(L, in, lim_addr, mis, hi, nb ? bcomp0 : s, s + 64 + LOOK);
-			const int32_t c = s + lane;
-			const Cand t = parse_cand(L.inb, mis, c, n, hi);
-			int32_t f = (t.kind == TK_NORMAL) ? t.next : (TERM | c);
-			int32_t fr[5];
-#pragma unroll
-			for (int r = 0; r < 5; ++r) {
-				fr[r] = f;
-				const bool inw = !(f & TERM) && f < s + 64;
-				const int32_t g = __shfl(f, inw ? f - s : lane);
-				f = inw ? g : f;
+			stage_to(L, in, lim_addr, mis, hi, pf, nb ? bcomp0 : s, s + 64 + LOOK);
+			STAMP(SP_STAGE);
+			STAMP_COUNT(SP_WINDOWS, 1);
+		}
+		// a literal run with a multi-byte extension will not fit a window:
+		// parse it serially from the ring instead of speculatively
+		const uint32_t peek = uint32_t(uni(int32_t(lds_u16(L.inb + ((s + mis) & INB_MASK)))));
+		if ((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) {
+			Cand t = {};
+			int32_t need = s + 2048;  // stage enough for long runs
+			if (need > n + 16)
+				need = n + 16;
+			const int32_t lo = nb ? bcomp0 : s;
+			bool okp = (need - lo) <= INB - 2048;
+			if (okp) {
+				stage_to(L, in, lim_addr, mis, hi, pf, lo, need);
+				okp = parse_serial(L.inb, mis, s, n, hi, t);
 			}
-			// lane j: position of the j-th token of the chain from s
-			int32_t cj = s;
+			const int32_t klen = t.L + t.ml;
+			const int32_t d0 = o + blen + t.L;
+			okp = okp && nb < MAXTOK && klen <= BIG && blen + klen <= OUTB &&
+			      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
+			      (t.off >= 16 || t.ml <= 64);
+#ifdef LZ4ADA_TRACE_POS
+			if (b == 0 && lane == 0 && o + blen <= LZ4ADA_TRACE_POS + 4096 && LZ4ADA_TRACE_POS < o + blen + 8192)
+				printf("[trace] serial s=%d okp=%d L=%d lit=%d off=%d ml=%d next=%d kind=%d nb=%d blen=%d o=%d hi=%d\n",
+				       s, int(okp), t.L, t.lit, t.off, t.ml, t.next, t.kind, nb, blen, o, hi);
+#endif
+			if (okp) {
+				if (lane == 0) {
+					L.r_tstart[nb] = blen;
+					L.r_L[nb] = t.L;
+					L.r_lit[nb] = t.lit;
+					L.r_off[nb] = t.off;
+					L.r_ml[nb] = t.ml;
+				}
+				if (nb == 0)
+					bcomp0 = s;
+				++nb;
+				blen += klen;
+				STAMP_COUNT(SP_TOKENS, 1);
+				if (t.kind == TK_LAST || t.next >= n) {
+					end_block = true;
+					s = t.next;
+				} else {
+					s = t.next;
+				}
+			} else if (nb == 0) {
+				stop = true;
+			} else {
+				force_flush = true;
+			}
+		} else {
+			// candidates at s + [0, WIN): next-token pointers
+#pragma unroll
+			for (int q = 0; q < WIN / 64; ++q) {
+				const int k = 64 * q + lane;
+				const Cand t = parse_cand(L.inb, mis, s + k, n);
+				const int32_t rel = t.next - s;
+				L.J[0][k] = uint16_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0xffff);
+			}
+			wave_lds_fence();
+			STAMP(SP_CAND);
+			// pointer doubling: J[r+1][k] = J[r][J[r][k]]
 #pragma unroll
 			for (int r = 0; r < 5; ++r) {
-				const bool inw = !(cj & TERM) && cj < s + 64;
-				const int32_t g = __shfl(fr[r], inw ? cj - s : 0);
+				uint32_t a[WIN / 64];
+#pragma unroll
+				for (int q = 0; q < WIN / 64; ++q)
+					a[q] = L.J[r][64 * q + lane];
+#pragma unroll
+				for (int q = 0; q < WIN / 64; ++q)
+					a[q] = a[q] < WIN ? L.J[r][a[q]] : 0xffffu;
+#pragma unroll
+				for (int q = 0; q < WIN / 64; ++q)
+					L.J[r + 1][64 * q + lane] = uint16_t(a[q]);
+				wave_lds_fence();
+			}
+			STAMP(SP_DOUBLE);
+			// lane j: window position of the j-th token of the chain from s
+			uint32_t cj = 0;
+#pragma unroll
+			for (int r = 0; r < 6; ++r) {
+				const uint32_t g = cj < WIN ? L.J[r][cj] : 0xffffu;
 				if ((lane >> r) & 1)
-					cj = inw ? g : cj;
+					cj = g;
 			}
-			const bool inwin = !(cj & TERM) && cj < s + 64 && lane < WTOK;
-			const int src = inwin ? cj - s : 0;
-			const int32_t kL = __shfl(t.L, src), klit = __shfl(t.lit, src);
-			const int32_t koff = __shfl(t.off, src), kml = __shfl(t.ml, src);
-			const int32_t knext = __shfl(t.next, src), kkind = __shfl(t.kind, src);
+			const bool inwin = cj < WIN;
+			const Cand tk = parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
+			const int32_t kL = tk.L, klit = tk.lit, koff = tk.off, kml = tk.ml;
+			const int32_t knext = tk.next, kkind = tk.kind;
 			const bool good = inwin && (kkind == TK_NORMAL || kkind == TK_LAST);
-			const int32_t klen = kL + (kkind == TK_NORMAL ? kml : 0);
-			// cut: capacity, long tokens, pre-block references, D5
-			const int32_t room_tok = MAXTOK - nb;
+			const int32_t klen = kL + kml;
 			const int32_t incl = wave_incl_scan(good ? klen : 0);
 			const int32_t tstart = blen + incl - klen;
 			const int32_t d0 = o + tstart + kL;  // block-relative match start
-			const bool fits = good && lane < room_tok && klen <= BIG && blen + incl <= OUTB &&
-			                  o + blen + incl <= cap && (kkind != TK_NORMAL || d0 - koff >= 0);
+			const bool fits = good && lane < MAXTOK - nb && klen <= BIG && blen + incl <= OUTB &&
+			                  o + blen + incl <= cap && (kkind != TK_NORMAL || d0 - koff >= 0) &&
+			                  (koff >= 16 || kml <= 64);
 			const uint64_t badm = __ballot(!fits);
 			const int cnt = badm ? (__ffsll((long long)badm) - 1) : 64;
-			// what comes after the taken tokens
 			const int32_t cnext = cnt > 0 ? __shfl(knext, cnt - 1) : s;
 			const int32_t ckind_last = cnt > 0 ? __shfl(kkind, cnt - 1) : TK_NORMAL;
 			if (lane < cnt) {
@@ -718,13 +931,19 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 				L.r_L[nb + lane] = kL;
 				L.r_lit[nb + lane] = klit;
 				L.r_off[nb + lane] = koff;
+				L.r_ml[nb + lane] = kml;
 			}
+			STAMP_COUNT(SP_TOKENS, cnt);
+#ifdef LZ4ADA_TRACE_POS
+			if (b == 0 && lane < cnt && o + tstart <= LZ4ADA_TRACE_POS + 4096 && LZ4ADA_TRACE_POS < o + tstart + 8192)
+				printf("[trace] window s=%d lane=%d cj=%u L=%d lit=%d off=%d ml=%d next=%d tstart=%d nb=%d o=%d\n",
+				       s, lane, cj, kL, klit, koff, kml, knext, tstart, nb, o);
+#endif
 			const bool was_empty = (nb == 0);
 			if (was_empty && cnt > 0)
 				bcomp0 = s;
-			const int32_t add = cnt > 0 ? __shfl(incl, cnt - 1) : 0;
 			nb += cnt;
-			blen += add;
+			blen += cnt > 0 ? __shfl(incl, cnt - 1) : 0;
 			if (cnt > 0 && ckind_last == TK_LAST) {
 				end_block = true;
 				s = n;
@@ -732,7 +951,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 				end_block = true;  // block ends right after a match (lz4ada.adb:780)
 				s = cnext;
 			} else if (cnt > 0) {
-				s = cnext;  // the chain continues; the next window starts there
+				s = cnext;
 			} else if (was_empty) {
 				stop = true;  // the token at s needs the one-token path
 			} else {
@@ -740,104 +959,110 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 			}
 		}
 		wave_lds_fence();
-		const bool flush = end_block || stop || force_flush || nb >= MAXTOK - 8 ||
+		STAMP(SP_SELECT);
+		const bool flush = end_block || stop || force_flush || nb > MAXTOK - WTOK / 2 ||
 		                   blen > OUTB - BIG || (s - bcomp0) >= SPAN;
 		if (flush && nb > 0) {
-			// ------------------------------------------- batch resolve
-			// token k lives in lane k
+			// -------------------------------------------- batch copy
 			const bool tl = lane < nb;
-			const int32_t k_ts = tl ? L.r_tstart[lane] : 0x7fffffff;
-			const int32_t k_L = tl ? L.r_L[lane] : 0;
-			const int32_t k_lit = tl ? L.r_lit[lane] : 0;
-			const int32_t k_off = tl ? L.r_off[lane] : 1;
-			for (int w = lane; w < OUTB / 32 + 2; w += 64)
-				L.starts[w] = 0u;
+			const int32_t ts = tl ? L.r_tstart[lane] : 0;
+			const int32_t tL = tl ? L.r_L[lane] : 0;
+			const int32_t tlit = tl ? L.r_lit[lane] : 0;
+			const int32_t toff = tl ? L.r_off[lane] : 1;
+			const int32_t tml = tl ? L.r_ml[lane] : 0;
+			// literals: ring -> batch buffer, exact length.  Short runs: one
+			// lane per token; long runs: the whole wave, one token at a time.
+			constexpr int32_t LONG = 48;
+			if (tL <= LONG) {
+				for (int32_t i = 0; i < tL; i += 16) {
+					u32x4 v;
+					__builtin_memcpy(&v, &L.inb[(tlit + i + mis) & INB_MASK], 16);
+					lds_store_n(&L.outb[ts + i], v, tL - i);
+				}
+			}
+			for (uint64_t lm = __ballot(tl && tL > LONG); lm; lm &= lm - 1) {
+				const int k = __ffsll((long long)lm) - 1;
+				const int32_t Lk = __shfl(tL, k), litk = __shfl(tlit, k), tsk = __shfl(ts, k);
+				for (int32_t i = 16 * lane; i < Lk; i += 1024) {
+					u32x4 v;
+					__builtin_memcpy(&v, &L.inb[(litk + i + mis) & INB_MASK], 16);
+					lds_store_n(&L.outb[tsk + i], v, Lk - i);
+				}
+			}
 			wave_lds_fence();
-			if (tl)
-				atomicOr(&L.starts[k_ts >> 5], 1u << (k_ts & 31));
-			wave_lds_fence();
-			// pass 1: each byte -> literal (compressed pos), pre-batch output
-			// pos (final after pass 2), or the earlier in-batch byte it copies
-			int32_t kbase = -1;
-			uint32_t pending = 0;  // chunks holding in-batch copies
-#pragma unroll 1
-			for (int32_t X = 0; X < blen; X += 64) {
-				const uint64_t m = uint64_t(L.starts[X >> 5]) |
-				                   (uint64_t(L.starts[(X >> 5) + 1]) << 32);
-				const uint64_t upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
-				int32_t k = kbase + __popcll(m & upto);
-				kbase += __popcll(m);
-				k = k < 0 ? 0 : (k >= nb ? nb - 1 : k);
-				const int32_t ts = __shfl(k_ts, k), tL = __shfl(k_L, k);
-				const int32_t tlit = __shfl(k_lit, k), toff = __shfl(k_off, k);
-				const int32_t x = X + lane;
-				bool inb_copy = false;
-				if (x < blen) {
-					int32_t fs = 0;
-					uint16_t ln = FINAL;
-					if (x < ts + tL) {
-						fs = ~(tlit + (x - ts));
+			STAMP(SP_LIT);
+			STAMP_COUNT(SP_BATCHES, 1);
+			// matches.  dep = earlier tokens whose match region overlaps this
+			// token's in-batch source range [a, b); a token copies in the
+			// first round in which none of them is pending.
+			const int32_t d0 = ts + tL;               // batch-relative
+			const int32_t q0 = o + d0 - toff;         // block-relative source
+			const int32_t sb = (q0 + tml < o + d0 ? q0 + tml : o + d0) - o;
+			const int32_t sa = (q0 - o > 0) ? q0 - o : 0;
+			const bool inbatch = tl && tml > 0 && sb > 0;
+			uint64_t dep = 0;
+			if (__ballot(inbatch)) {
+				const int32_t ka = owner_of(ts, nb, inbatch ? sa : 0);
+				const int32_t kb = owner_of(ts, nb, inbatch ? sb - 1 : 0);
+				const int32_t d0_ka = __shfl(d0, ka), ml_ka = __shfl(tml, ka);
+				const int32_t d0_kb = __shfl(d0, kb), ml_kb = __shfl(tml, kb);
+				if (inbatch) {
+					if (kb > ka + 1)
+						dep = ((1ull << kb) - 1) & ~((2ull << ka) - 1);
+					if (ml_ka > 0 && d0_ka < sb && d0_ka + ml_ka > sa)
+						dep |= 1ull << ka;
+					if (kb != ka && ml_kb > 0 && d0_kb < sb)
+						dep |= 1ull << kb;
+					dep &= (1ull << lane) - 1;  // own literals are final already
+				}
+			}
+			bool pend = tl && tml > 0;
+			for (int guard = 0; ; ++guard) {
+				const uint64_t pm = __ballot(pend);
+				if (!pm)
+					break;
+				const bool ready = pend && (!(pm & dep) || guard > MAXTOK);
+#ifdef LZ4ADA_TRACE_POS
+				if (ready && b == 0 && o + d0 <= LZ4ADA_TRACE_POS && LZ4ADA_TRACE_POS < o + d0 + tml)
+					printf("[trace] match lane=%d o=%d ts=%d tL=%d d0=%d off=%d ml=%d q0=%d nb=%d blen=%d guard=%d\n",
+					       lane, o, ts, tL, d0, toff, tml, q0, nb, blen, guard);
+#endif
+				if (ready) {
+					if (toff >= 16) {
+						// 16-byte chunks; a chunk's source ends before its
+						// destination starts, so own output is already there
+						for (int32_t i = 0; i < tml; i += 16) {
+							const int32_t sp = q0 + i;
+							const int32_t nn = tml - i < 16 ? tml - i : 16;
+							u32x4 v;
+							if (sp + 16 <= o) {
+								__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
+							} else if (sp >= o) {
+								__builtin_memcpy(&v, &L.outb[sp - o], 16);
+							} else {
+								uint8_t t[16];
+								for (int k = 0; k < 16; ++k)
+									t[k] = (sp + k < o) ? ob[sp + k] : L.outb[sp + k - o];
+								__builtin_memcpy(&v, t, 16);
+							}
+							lds_store_n(&L.outb[d0 + i], v, nn);
+						}
 					} else {
-						const int32_t j = x - (ts + tL);
-						const int32_t srcp = o + ts + tL - toff + (j < toff ? j : j % toff);
-						if (srcp < o) {
-							fs = srcp;
-						} else {
-							ln = uint16_t(srcp - o);
-							inb_copy = true;
+						// short offset: byte k repeats source byte (k mod off)
+						int32_t r = 0;
+						for (int32_t k = 0; k < tml; ++k) {
+							const int32_t sp = q0 + r;
+							L.outb[d0 + k] = (sp < o) ? ob[sp] : L.outb[sp - o];
+							if (++r == toff)
+								r = 0;
 						}
 					}
-					L.fsrc[x] = fs;
-					L.link[x] = ln;
 				}
-				if (__ballot(inb_copy))
-					pending |= 1u << (X >> 6);
+				pend = pend && !ready;
+				wave_lds_fence();
+				STAMP_COUNT(SP_ROUNDS, 1);
 			}
-			wave_lds_fence();
-			// pass 2: fetch every final byte; 8 chunks of loads in flight
-#pragma unroll 1
-			for (int32_t X = 0; X < blen; X += 512) {
-				int32_t fv[8];
-				uint32_t gv[8], lv[8];
-#pragma unroll
-				for (int u = 0; u < 8; ++u) {
-					const int32_t x = X + 64 * u + lane;
-					fv[u] = (x < blen) ? L.fsrc[x] : 0;
-				}
-#pragma unroll
-				for (int u = 0; u < 8; ++u)
-					gv[u] = ob[fv[u] >= 0 ? fv[u] : 0];
-#pragma unroll
-				for (int u = 0; u < 8; ++u)
-					lv[u] = L.inb[((fv[u] < 0 ? ~fv[u] : 0) + mis) & INB_MASK];
-#pragma unroll
-				for (int u = 0; u < 8; ++u) {
-					const int32_t x = X + 64 * u + lane;
-					if (x < blen && L.link[x] == FINAL)
-						L.outb[x] = uint8_t(fv[u] >= 0 ? gv[u] : lv[u]);
-				}
-			}
-			wave_lds_fence();
-			// pass 3: in-batch copies read the final byte at the end of
-			// their link chain (every link points strictly backwards)
-			while (pending) {
-				const int ch = __ffs(pending) - 1;
-				pending &= pending - 1;
-				const int32_t x = ch * 64 + lane;
-				if (x < blen) {
-					uint32_t y = L.link[x];
-					if (y != FINAL) {
-						for (int guard = 0; guard <= OUTB; ++guard) {
-							const uint32_t z = L.link[y];
-							if (z == FINAL)
-								break;
-							y = z;
-						}
-						L.outb[x] = L.outb[y];
-					}
-				}
-			}
-			__syncthreads();
+			STAMP(SP_MATCH);
 			// flush the batch to HBM
 			{
 				g8* dst = ob + o;
@@ -854,7 +1079,12 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 				for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)
 					dst[i] = L.outb[i];
 			}
-			__syncthreads();
+			__syncthreads();  // HBM writes visible to this wave's later loads
+#ifdef LZ4ADA_TRACE_POS
+			if (b == 0 && lane == 0 && o <= LZ4ADA_TRACE_POS + 4096 && LZ4ADA_TRACE_POS < o + blen + 4096)
+				printf("[trace] flush o=%d blen=%d nb=%d bcomp0=%d s=%d hi=%d\n", o, blen, nb, bcomp0, s, hi);
+#endif
+			STAMP(SP_FLUSH);
 			o += blen;
 			nb = 0;
 			blen = 0;
@@ -872,8 +1102,10 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 				if (s >= n)
 					done = true;
 			}
+			STAMP(SP_ONE);
 		}
 	}
+	STAMP_FLUSH();
 
 	if (lane == 0) {
 		status[b].code = ok ? int32_t(DS_OK) : st.code;
@@ -1105,6 +1337,21 @@ __global__ __launch_bounds__(64) void k_serial_block(uint8_t* buf, int64_t bufle
 }
 
 // -------------------------------------------------------------- launchers
+
+#ifdef LZ4ADA_STAMPS
+extern "C" int lz4ada_debug_stamps(unsigned long long* out, int reset)
+{
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * SP_N) !=
+	    hipSuccess)
+		return -1;
+	if (reset) {
+		unsigned long long z[SP_N] = {};
+		if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess)
+			return -1;
+	}
+	return SP_N;
+}
+#endif
 
 hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,

@@ -28,7 +28,8 @@ except Exception:  # torch is optional for this binding
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblz4ada_hip.so")
+# LZ4ADA_LIB selects a diagnostic build (tools/stamps.py); default: the product.
+LIB_PATH = os.environ.get("LZ4ADA_LIB") or os.path.join(_HERE, "liblz4ada_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} is missing: build it with `make -C bo-lz4-ada_amd/csrc` "

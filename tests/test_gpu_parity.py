@@ -224,3 +224,38 @@ def test_device_resident_blocks():
         if descs[i].flags & lz4ada.BLOCK_HAS_CKSUM:
             assert st[i].cksum == descs[i].cksum
     assert bytes(d_out.cpu().numpy()[:total]) == raw
+
+
+# ------------------------------------------- bench-sized blocks (regression)
+
+@pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
+def test_bench_blocks_exact(kind):
+    """The bench's own unique 4 MiB blocks (seed 0x4C5A3441 + i) decode
+    byte-exactly through the device-resident path."""
+    torch = pytest.importorskip("torch")
+    seeds = [0x4C5A3441 + i for i in range(16)]
+    bmax = 4 << 20
+    blocks = [lz4ada.gen_block(lz4ada.GEN_KINDS[kind], sd, bmax) for sd in seeds]
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax,
+                                      block_cksum=True)
+    info, descs = lz4ada.frame_index(frame)
+    nb = info.nblocks
+    dev = torch.device("cuda:0")
+    d_frame = torch.frombuffer(bytearray(frame), dtype=torch.uint8).to(dev)
+    d_desc = torch.frombuffer(bytearray(bytes(descs)[:nb * 32]), dtype=torch.uint8).to(dev)
+    d_out = torch.zeros(nb * bmax, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
+    lz4ada.decode_blocks_device(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
+                                d_out.data_ptr(), d_st.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    st = (lz4ada.BlockStatus * nb).from_buffer_copy(d_st.cpu().numpy().tobytes())
+    out = d_out.cpu().numpy().tobytes()
+    bad = []
+    for i, (c, r) in enumerate(blocks):
+        got = out[i * bmax:i * bmax + len(r)]
+        if st[i].code or st[i].out_len != len(r) or got != r:
+            j = next((k for k in range(len(r)) if got[k] != r[k]), -1)
+            bad.append((i, st[i].code, st[i].out_len, j,
+                        got[max(j - 8, 0):j + 8].hex(), r[max(j - 8, 0):j + 8].hex()))
+    assert not bad, bad
