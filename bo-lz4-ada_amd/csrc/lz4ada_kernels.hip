@@ -305,6 +305,10 @@ constexpr int MAXTOK = 64;       // tokens per batch (one per lane)
 constexpr int WTOK = 64;         // tokens taken from one window (one per lane)
 constexpr int BIG = 1024;        // longer sequences take the one-token path
 constexpr int SPAN = 2048;       // compressed bytes a batch may span
+constexpr int STAGE_AHEAD = 2112;  // staged bytes kept ahead of the chain (>= 64 + LOOK, > BIG)
+static_assert(STAGE_AHEAD >= 64 + LOOK && STAGE_AHEAD > BIG + 16, "staging lead too short");
+// ring occupancy bound: batch span + one token's advance + lead + chunk
+static_assert(SPAN + BIG + 64 + STAGE_AHEAD + 1024 + 16 <= INB, "input ring too small");
 
 enum TokKind : int { TK_NORMAL = 0, TK_LAST = 1, TK_COMPLEX = 2, TK_ERR = 3 };
 
@@ -708,21 +712,24 @@ __device__ __forceinline__ u32x4 load_chunk(cg8* in, uintptr_t lim_addr, int32_t
 }
 
 __device__ __forceinline__ void stage_to(DecLds& L, cg8* in, uintptr_t lim_addr, int32_t mis,
-                                         int32_t& hi, u32x4& pf, int32_t lo, int32_t need)
+                                         int32_t& hi, u32x4& pf0, u32x4& pf1, int32_t lo,
+                                         int32_t need)
 {
 	const uint32_t lane = lane_id();
 	if (hi < lo) {  // jumped ahead (one-token path): restart the stream at lo
 		hi = ((lo + mis) & ~15) - mis;
-		pf = load_chunk(in, lim_addr, hi);
+		pf0 = load_chunk(in, lim_addr, hi);
+		pf1 = load_chunk(in, lim_addr, hi + 1024);
 	}
 	bool any = false;
 	while (hi < need) {
 		const uint32_t idx = uint32_t(hi + mis + 16 * int32_t(lane)) & INB_MASK;
-		*reinterpret_cast<u32x4*>(&L.inb[idx]) = pf;
+		*reinterpret_cast<u32x4*>(&L.inb[idx]) = pf0;
 		if (idx == 0)
-			*reinterpret_cast<u32x4*>(&L.inb[INB]) = pf;  // mirror for wrap-free reads
+			*reinterpret_cast<u32x4*>(&L.inb[INB]) = pf0;  // mirror for wrap-free reads
 		hi += 1024;
-		pf = load_chunk(in, lim_addr, hi);  // next chunk in flight
+		pf0 = pf1;
+		pf1 = load_chunk(in, lim_addr, hi + 1024);  // two chunks in flight
 		any = true;
 	}
 	if (any)
@@ -806,7 +813,8 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 	int32_t s = 0;       // block-relative compressed position of the chain
 	int32_t o = 0;       // block-relative output position (flushed)
 	int32_t hi = -mis;   // staged compressed bytes end (block-relative)
-	u32x4 pf = load_chunk(in, lim_addr, hi);
+	u32x4 pf0 = load_chunk(in, lim_addr, hi);
+	u32x4 pf1 = load_chunk(in, lim_addr, hi + 1024);
 	int32_t nb = 0;      // tokens in the current batch
 	int32_t blen = 0;    // batch output bytes
 	int32_t bcomp0 = 0;  // compressed position of the batch's first token
@@ -823,7 +831,9 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 		// ------------------------------------------------ window parse at s
 		bool stop = false, end_block = false, force_flush = false;
 		{
-			stage_to(L, in, lim_addr, mis, hi, pf, nb ? bcomp0 : s, s + 64 + LOOK);
+			// keep the ring ahead of the chain: a window needs s + 64 + LOOK,
+			// a serial long-literal token up to s + BIG + 16
+			stage_to(L, in, lim_addr, mis, hi, pf0, pf1, nb ? bcomp0 : s, s + STAGE_AHEAD);
 			STAMP(SP_STAGE);
 			STAMP_COUNT(SP_WINDOWS, 1);
 		}
@@ -832,15 +842,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 		const uint32_t peek = uint32_t(uni(int32_t(lds_u16(L.inb + ((s + mis) & INB_MASK)))));
 		if ((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) {
 			Cand t = {};
-			int32_t need = s + 2048;  // stage enough for long runs
-			if (need > n + 16)
-				need = n + 16;
-			const int32_t lo = nb ? bcomp0 : s;
-			bool okp = (need - lo) <= INB - 2048;
-			if (okp) {
-				stage_to(L, in, lim_addr, mis, hi, pf, lo, need);
-				okp = parse_serial(L.inb, mis, s, n, hi, t);
-			}
+			bool okp = parse_serial(L.inb, mis, s, n, hi, t);
 			const int32_t klen = t.L + t.ml;
 			const int32_t d0 = o + blen + t.L;
 			okp = okp && nb < MAXTOK && klen <= BIG && blen + klen <= OUTB &&
@@ -970,6 +972,18 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 			const int32_t tlit = tl ? L.r_lit[lane] : 0;
 			const int32_t toff = tl ? L.r_off[lane] : 1;
 			const int32_t tml = tl ? L.r_ml[lane] : 0;
+			// first 32 bytes of every pre-batch match source: loads issued now,
+			// consumed in the match rounds, so their latency hides under the
+			// literal copy
+			const int32_t d0 = ts + tL;               // batch-relative
+			const int32_t q0 = o + d0 - toff;         // block-relative source
+			u32x4 pv0 = {0, 0, 0, 0}, pv1 = {0, 0, 0, 0};
+			const bool pre0 = tl && tml > 0 && toff >= 16 && q0 + 16 <= o;
+			const bool pre1 = pre0 && tml > 16 && q0 + 32 <= o;
+			if (pre0)
+				__builtin_memcpy(&pv0, (const uint8_t*)(ob + q0), 16);
+			if (pre1)
+				__builtin_memcpy(&pv1, (const uint8_t*)(ob + q0 + 16), 16);
 			// literals: ring -> batch buffer, exact length.  Short runs: one
 			// lane per token; long runs: the whole wave, one token at a time.
 			constexpr int32_t LONG = 48;
@@ -995,8 +1009,6 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 			// matches.  dep = earlier tokens whose match region overlaps this
 			// token's in-batch source range [a, b); a token copies in the
 			// first round in which none of them is pending.
-			const int32_t d0 = ts + tL;               // batch-relative
-			const int32_t q0 = o + d0 - toff;         // block-relative source
 			const int32_t sb = (q0 + tml < o + d0 ? q0 + tml : o + d0) - o;
 			const int32_t sa = (q0 - o > 0) ? q0 - o : 0;
 			const bool inbatch = tl && tml > 0 && sb > 0;
@@ -1035,7 +1047,11 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 							const int32_t sp = q0 + i;
 							const int32_t nn = tml - i < 16 ? tml - i : 16;
 							u32x4 v;
-							if (sp + 16 <= o) {
+							if (i == 0 && pre0) {
+								v = pv0;
+							} else if (i == 16 && pre1) {
+								v = pv1;
+							} else if (sp + 16 <= o) {
 								__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
 							} else if (sp >= o) {
 								__builtin_memcpy(&v, &L.outb[sp - o], 16);
