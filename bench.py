@@ -117,7 +117,7 @@ def cpu_baseline(recs, block_max, budget_s):
     st, out, msg = O.unlz4ada(f1, out_cap=len(raw1) + MiB)
     t1 = time.perf_counter() - t0
     assert st == O.OK and out == raw1, msg
-    k = max(1, min(len(recs) * 4, int(budget_s / max(t1, 1e-6))))
+    k = max(1, min(2048, int(budget_s / max(t1, 1e-6))))
     fk, rawk = frame_of(k)
     t0 = time.perf_counter()
     st, out, msg = O.unlz4ada(fk, out_cap=len(rawk) + MiB)

@@ -259,3 +259,26 @@ def test_bench_blocks_exact(kind):
             bad.append((i, st[i].code, st[i].out_len, j,
                         got[max(j - 8, 0):j + 8].hex(), r[max(j - 8, 0):j + 8].hex()))
     assert not bad, bad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_decode_each_rank_share(world):
+    """shard.decode_frame_sharded for every rank of a world (no process group:
+    the status reduce is local), reassembled against the oracle."""
+    import shard
+    import torch
+    blocks = []
+    for i in range(7):
+        raw_len = 256 * 1024 if i < 6 else 1000
+        comp, raw = lz4ada.gen_block(i % 4, 0x4C5A3441 + i, raw_len)
+        blocks.append((comp, raw, False))
+    frame, expected = lz4frame.build_frame(blocks, 256 * 1024, indep=True, block_cksum=True)
+    got = b""
+    for rank in range(world):
+        d_out, (lo, hi), lens = shard.decode_frame_sharded(frame, rank, world,
+                                                          torch.device("cuda", 0))
+        host = d_out.cpu().numpy().tobytes()
+        for j, ln in enumerate(lens):
+            got += host[j * 256 * 1024:j * 256 * 1024 + ln]
+    assert got == expected

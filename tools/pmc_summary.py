@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into profiles/.
+
+    python tools/pmc_summary.py gpurun_out/prof_r01 r01 [--kind mixed --blocks 2048]
+
+Writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>_pmc.json           per-kernel counters, averaged per dispatch
+  profiles/pmc_decode.json          HBM bytes per k_decode_blocks launch, read by bench.py
+
+HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3):
+FETCH_SIZE and WRITE_SIZE are in KiB, collected in separate --pmc passes;
+on gfx950 FETCH_SIZE reports half the bytes of 16-byte-per-lane streaming
+reads, so it is doubled; WRITE_SIZE is exact for 16-byte-per-lane stores.
+Both count L2 misses served by the Infinity Cache as well as HBM.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = ("k_decode_blocks", "k_block_checksums", "k_output_checksums", "k_serial_block",
+           "k_xxh32_update", "k_compact")
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("tag")
+    ap.add_argument("--kind", default="mixed")
+    ap.add_argument("--blocks", type=int, default=2048)
+    ap.add_argument("--block-max", type=int, default=4 << 20)
+    args = ap.parse_args()
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+
+    stats = os.path.join(args.dir, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(prof, f"{args.tag}_kernel_stats.csv"))
+    avg_ns = {}
+    with open(stats) as fh:
+        for r in csv.DictReader(fh):
+            k = short(r["Name"])
+            if k:
+                avg_ns[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+
+    counters = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(args.dir, "pmc*", "run_counter_collection.csv"))):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                k = short(r["Kernel_Name"])
+                if k:
+                    counters[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    per = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in counters.items()}
+
+    out = {"tag": args.tag, "kernels": {}}
+    for k in sorted(set(avg_ns) | set(per)):
+        e = dict(avg_ns.get(k, {}))
+        e["counters_per_dispatch"] = per.get(k, {})
+        c = per.get(k, {})
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            e["fetch_bytes_raw"] = c["FETCH_SIZE"] * 1024
+            e["fetch_bytes_x2"] = c["FETCH_SIZE"] * 1024 * 2
+            e["write_bytes"] = c["WRITE_SIZE"] * 1024
+            e["hbm_bytes_per_launch"] = e["fetch_bytes_x2"] + e["write_bytes"]
+        if "SQ_WAVE_CYCLES" in c:
+            wc = c["SQ_WAVE_CYCLES"]
+            e["issue_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0) / wc
+            e["wait_frac"] = c.get("SQ_WAIT_ANY", 0) / wc
+        insts = sum(c.get(n, 0) for n in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
+                                          "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                                          "SQ_INSTS_BRANCH"))
+        if insts:
+            e["wave_instructions"] = insts
+        out["kernels"][k] = e
+    with open(os.path.join(prof, f"{args.tag}_pmc.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+    dec = out["kernels"].get("k_decode_blocks", {})
+    if "hbm_bytes_per_launch" in dec:
+        pj = {"config": {"kind": args.kind, "blocks": args.blocks, "block_max": args.block_max},
+              "hbm_bytes_per_launch": round(dec["hbm_bytes_per_launch"]),
+              "fetch_bytes_x2": round(dec["fetch_bytes_x2"]),
+              "write_bytes": round(dec["write_bytes"]),
+              "avg_ns": dec.get("avg_ns"),
+              "source": f"profiles/{args.tag}_pmc.json (tools/profile.sh + tools/pmc_summary.py)"}
+        with open(os.path.join(prof, "pmc_decode.json"), "w") as fh:
+            json.dump(pj, fh, indent=1)
+    print(json.dumps({k: {kk: v for kk, v in e.items() if kk != "counters_per_dispatch"}
+                      for k, e in out["kernels"].items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
