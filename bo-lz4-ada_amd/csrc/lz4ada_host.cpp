@@ -1121,6 +1121,17 @@ int lz4ada_launch_decode(const void* d_frame, uint64_t frame_len, const lz4ada_b
 	});
 }
 
+int lz4ada_launch_decode_wg(const void* d_frame, uint64_t frame_len,
+                            const lz4ada_block_desc* d_descs, int64_t nblocks, void* d_out,
+                            lz4ada_block_status* d_status, void* stream)
+{
+	return guarded(nullptr, [&] {
+		HIP_OK(launch_decode_wg(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
+		                        uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,
+		                        static_cast<hipStream_t>(stream)));
+	});
+}
+
 int lz4ada_launch_block_checksums(const void* d_frame, const lz4ada_block_desc* d_descs,
                                   int64_t nblocks, lz4ada_block_status* d_status, void* stream)
 {

@@ -31,6 +31,7 @@ enum DevStatus : int32_t {
 	DS_BACKREF = 7,        // lz4ada.adb:867-874 (detail = H_Offset)
 	DS_CONTENT_SIZE = 8,   // lz4ada.adb:830-835
 	DS_INTERNAL = 9,       // decoder invariant broken (never expected)
+	DS_RETRY = 10,         // k_decode_wg declined the block: k_decode_blocks redoes it
 };
 
 // State of the serial reference-exact block kernel (emulates one
@@ -50,11 +51,19 @@ struct SerialState {
 // ---- launchers (lz4ada_kernels.hip) ----
 // All launch on `stream` and never synchronise.
 
-// Bulk independent-block decode: one wavefront per block.
+// Bulk independent-block decode: k_decode_blocks (one wavefront per
+// block).  LZ4ADA_DECODER=wg runs k_decode_wg (workgroup per block) first
+// and k_decode_blocks only for the blocks it declined.
 hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                 uint8_t* d_out, lz4ada_block_status* d_status,
                                 hipStream_t stream);
+
+// Workgroup-per-block decoder alone (lz4ada_wg.hip); declined blocks get
+// status DS_RETRY.
+hipError_t launch_decode_wg(const uint8_t* d_frame, uint64_t frame_len,
+                            const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
+                            lz4ada_block_status* d_status, hipStream_t stream);
 
 // Per-block XXH32 of the compressed payloads (block checksums).
 hipError_t launch_block_checksums(const uint8_t* d_frame,

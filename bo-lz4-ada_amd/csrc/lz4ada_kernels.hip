@@ -30,54 +30,18 @@
 //    streaming Update facade and by the bulk path's exact fallback.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "lz4ada_internal.h"
+#include "lz4ada_dev.h"
 
 namespace lz4ada {
 
-// Device code addresses HBM through address_space(1) pointers so that every
-// access is a global_* instruction (a generic pointer becomes flat_*, which
-// also ticks lgkmcnt and forces extra waits).
-#define GLOBAL __attribute__((address_space(1)))
-typedef const GLOBAL uint8_t cg8;
-typedef GLOBAL uint8_t g8;
-typedef const GLOBAL uint32_t cg32;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-template <class T>
-__device__ __forceinline__ const GLOBAL T* gptr(const T* p)
-{
-	return (const GLOBAL T*)(p);
-}
-template <class T>
-__device__ __forceinline__ GLOBAL T* gptr(T* p)
-{
-	return (GLOBAL T*)(p);
-}
 
 // ------------------------------------------------------------------ XXH32
 
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r)
-{
-	return (x << r) | (x >> (32 - r));
-}
 
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
-// Unaligned little-endian dword from global memory.  Reads only the aligned
-// dwords that contain wanted bytes, so it never touches a page the data
-// does not.
-__device__ __forceinline__ uint32_t ld32u_cached(cg8* p)
-{
-	uintptr_t a = reinterpret_cast<uintptr_t>(p);
-	cg32* q = reinterpret_cast<cg32*>(a & ~uintptr_t(3));
-	uint32_t sh = uint32_t(a & 3u);
-	uint32_t lo = q[0];
-	if (sh == 0)
-		return lo;
-	uint32_t hi = q[1];
-	return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
 
 constexpr int XR = 16;  // dwords per lane per step (4 KiB per wave)
 
@@ -351,18 +315,6 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v)
 	return v;
 }
 
-// Inclusive prefix sum over the wave with DPP (row_shr within 16-lane rows,
-// then row_bcast:15 / row_bcast:31 across rows) -- VALU latency, no LDS.
-__device__ __forceinline__ int32_t wave_incl_scan(int32_t v)
-{
-	v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);  // row_shr:1
-	v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);  // row_shr:2
-	v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);  // row_shr:4
-	v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);  // row_shr:8
-	v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); // row_bcast:15
-	v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); // row_bcast:31
-	return v;
-}
 
 // Sum of a length extension (Process_Variable_Length, lz4ada.adb:724-735)
 // starting at block-relative p, 64 bytes per step.  Returns false when the
@@ -677,7 +629,7 @@ __device__ __forceinline__ int32_t owner_of(int32_t ts_reg, int32_t nb, int32_t 
 	return lo;
 }
 
-struct DecLds {
+struct alignas(16) DecLds {
 	uint16_t J[6][WIN];         // J[r][k]: window position 2^r tokens after k (>= WIN: out)
 	uint8_t inb[INB + MIRROR];  // block-relative x -> inb[(x + mis) & INB_MASK]
 	uint8_t outb[OUTB + 32];    // batch output
@@ -690,7 +642,6 @@ struct DecLds {
 
 // Cross-lane hand-off through LDS inside one wavefront: LDS executes a
 // wave's operations in order, so only the compiler must not reorder.
-__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
 
 // Stage compressed bytes so that block-relative [lo, need) is in the ring.
 // `pf` holds the 1 KiB chunk at `hi`, loaded ahead; writing it to LDS is
@@ -737,45 +688,20 @@ __device__ __forceinline__ void stage_to(DecLds& L, cg8* in, uintptr_t lim_addr,
 }
 
 // Exact-length store of n (0..16) bytes of v to LDS.
-__device__ __forceinline__ void lds_store_n(uint8_t* dst, u32x4 v, int32_t n)
-{
-	if (n >= 16) {
-		__builtin_memcpy(dst, &v, 16);
-		return;
-	}
-	uint64_t lo = uint64_t(v.x) | (uint64_t(v.y) << 32);
-	uint64_t hi = uint64_t(v.z) | (uint64_t(v.w) << 32);
-	if (n & 8) {
-		__builtin_memcpy(dst, &lo, 8);
-		dst += 8;
-		lo = hi;
-	}
-	if (n & 4) {
-		const uint32_t x = uint32_t(lo);
-		__builtin_memcpy(dst, &x, 4);
-		dst += 4;
-		lo >>= 32;
-	}
-	if (n & 2) {
-		const uint16_t x = uint16_t(lo);
-		__builtin_memcpy(dst, &x, 2);
-		dst += 2;
-		lo >>= 16;
-	}
-	if (n & 1)
-		*dst = uint8_t(lo);
-}
 
 __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict__ frame,
                                                        uint64_t frame_len,
                                                        const lz4ada_block_desc* __restrict__ desc,
                                                        uint32_t nblocks, uint8_t* __restrict__ out,
-                                                       lz4ada_block_status* __restrict__ status)
+                                                       lz4ada_block_status* __restrict__ status,
+                                                       int retry_only)
 {
 	__shared__ DecLds L;
 
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
+		return;
+	if (retry_only && status[b].code != DS_RETRY)
 		return;
 	const int lane = int(lane_id());
 	const lz4ada_block_desc d = desc[b];
@@ -1376,8 +1302,20 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
 {
 	if (nblocks == 0)
 		return hipSuccess;
+	// LZ4ADA_DECODER=wg: workgroup decoder first (experimental; the
+	// per-wave decoder is faster on every content class measured so far)
+	static const int wave_only = [] {
+		const char* e = getenv("LZ4ADA_DECODER");
+		return (e && e[0] == 'w' && e[1] == 'g') ? 0 : 1;
+	}();
+	if (!wave_only) {
+		const hipError_t err = launch_decode_wg(d_frame, frame_len, d_desc, nblocks, d_out,
+		                                        d_status, stream);
+		if (err != hipSuccess)
+			return err;
+	}
 	hipLaunchKernelGGL(k_decode_blocks, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
-	                   d_desc, nblocks, d_out, d_status);
+	                   d_desc, nblocks, d_out, d_status, wave_only ? 0 : 1);
 	return hipGetLastError();
 }
 

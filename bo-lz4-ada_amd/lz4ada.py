@@ -183,6 +183,7 @@ _sig = {
     "lz4ada_decode_blocks_device": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp],
                                     ctypes.c_int),
     "lz4ada_launch_decode": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp], ctypes.c_int),
+    "lz4ada_launch_decode_wg": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lz4ada_launch_block_checksums": ([_vp, _vp, _i64, _vp, _vp], ctypes.c_int),
     "lz4ada_output_checksums_device": ([_vp, _vp, _vp, _i64, _vp, _vp], ctypes.c_int),
     "lz4ada_decode_frame": ([_vp, _i64, _vp, _i64, _pi64, _pi64], ctypes.c_int),
@@ -372,6 +373,15 @@ def decode_blocks_device(d_frame: int, frame_len: int, d_descs: int, nblocks: in
 def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=0):
     _check(_lib.lz4ada_launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status,
                                      stream), _thread_error())
+
+
+def launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=0):
+    """Workgroup-per-block decoder alone; declined blocks keep status DS_RETRY."""
+    _check(_lib.lz4ada_launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status,
+                                        stream), _thread_error())
+
+
+DS_RETRY = 10
 
 
 def launch_block_checksums(d_frame, d_descs, nblocks, d_status, stream=0):

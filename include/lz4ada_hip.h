@@ -207,6 +207,12 @@ int lz4ada_decode_blocks_device(const void *d_frame, uint64_t frame_len,
 int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
                          const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                          lz4ada_block_status *d_status, void *stream);
+/* The workgroup-per-block decoder alone: blocks it declines (malformed
+ * data, oversize sequences) keep status code 10 (retry) and are not
+ * decoded; lz4ada_launch_decode runs it and then redoes those blocks. */
+int lz4ada_launch_decode_wg(const void *d_frame, uint64_t frame_len,
+                            const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
+                            lz4ada_block_status *d_status, void *stream);
 int lz4ada_launch_block_checksums(const void *d_frame, const lz4ada_block_desc *d_descs,
                                   int64_t nblocks, lz4ada_block_status *d_status,
                                   void *stream);
