@@ -127,4 +127,34 @@ __device__ __forceinline__ u32x4 ld16u(const uint8_t* base, uint32_t a, uint32_t
 	return v;
 }
 
+// Period-off (< 16) match pattern: from the off source bytes (s0 = bytes
+// 0..7, s1 = bytes 8..15 of the source window) build the phase-0 pattern
+// pv; storing it every *stp bytes (*width bytes per store, the last store
+// clipped) writes the whole match -- overlapping stores write equal bytes.
+__device__ __forceinline__ void make_pattern(uint64_t s0, uint64_t s1, int32_t off, u32x4& pv,
+                                             int32_t& width, int32_t& stp)
+{
+	if (off <= 8) {
+		uint64_t x = off == 8 ? s0 : (s0 & ((uint64_t(1) << (8 * off)) - 1));
+		for (int32_t w = off; w < 8; w <<= 1)
+			x |= x << (8 * w);
+		pv.x = uint32_t(x);
+		pv.y = uint32_t(x >> 32);
+		pv.z = pv.x;
+		pv.w = pv.y;
+		width = 8;
+		stp = off * (8 / off);
+	} else {
+		// bytes 0..off-1 = source, off..15 = source bytes 0..15-off
+		const int32_t r = off - 8;
+		const uint64_t hi = (s1 & ((uint64_t(1) << (8 * r)) - 1)) | (s0 << (8 * r));
+		pv.x = uint32_t(s0);
+		pv.y = uint32_t(s0 >> 32);
+		pv.z = uint32_t(hi);
+		pv.w = uint32_t(hi >> 32);
+		width = 16;
+		stp = off;
+	}
+}
+
 }  // namespace lz4ada

@@ -906,10 +906,12 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 			u32x4 pv0 = {0, 0, 0, 0}, pv1 = {0, 0, 0, 0};
 			const bool pre0 = tl && tml > 0 && toff >= 16 && q0 + 16 <= o;
 			const bool pre1 = pre0 && tml > 16 && q0 + 32 <= o;
+#ifndef LZ4ADA_EXP_NOGLOBAL
 			if (pre0)
 				__builtin_memcpy(&pv0, (const uint8_t*)(ob + q0), 16);
 			if (pre1)
 				__builtin_memcpy(&pv1, (const uint8_t*)(ob + q0 + 16), 16);
+#endif
 			// literals: ring -> batch buffer, exact length.  Short runs: one
 			// lane per token; long runs: the whole wave, one token at a time.
 			constexpr int32_t LONG = 48;
@@ -978,7 +980,11 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 							} else if (i == 16 && pre1) {
 								v = pv1;
 							} else if (sp + 16 <= o) {
+#ifdef LZ4ADA_EXP_NOGLOBAL
+								v = pv0;
+#else
 								__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
+#endif
 							} else if (sp >= o) {
 								__builtin_memcpy(&v, &L.outb[sp - o], 16);
 							} else {

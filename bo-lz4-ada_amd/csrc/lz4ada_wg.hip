@@ -44,43 +44,40 @@ constexpr int REG = 32;                     // compressed bytes per lane region
 constexpr int BATCH_IN = LANES * REG;       // 16 KiB compressed per batch
 constexpr int IN_OVH = 1024;                // staged bytes past the batch
 constexpr int IN_STAGE = BATCH_IN + IN_OVH + 32;
-constexpr int RING = 96 * 1024;             // output ring: 64 KiB history + batch
+constexpr int RING = 96 * 1024;             // output ring: 64 KiB window + a batch
 constexpr int OUT_CAP = 32 * 1024;          // output bytes per batch
-constexpr int HIST = 65536;
-static_assert(RING >= HIST + OUT_CAP, "ring must hold the window and a batch");
-constexpr int CMAX = 96;                    // continuation steps before a batch is cut
+constexpr int RING_HIST = RING - OUT_CAP;   // history bytes always still in the ring
+static_assert(RING_HIST >= 65536, "every match source stays in the ring");
+constexpr int CMAX = 48;                    // continuation steps before a batch is cut
+constexpr int LONG = 64;                    // longer literal/match runs: whole-wave copies
 constexpr int NDONE = OUT_CAP / 32 + 1;     // done-bitmap words
+constexpr int MAXTOK = 4096;                // sequences per batch
 constexpr int TERM = LANES;                 // path terminal node
 constexpr int LEVELS = 9;                   // log2(LANES)
 static_assert((1 << LEVELS) == LANES, "doubling levels");
+static_assert(REG == 32, "vis masks are 32-bit");
 
 // link types of a lane's continuation
 enum Link : uint8_t { LK_LANE = 0, LK_END = 1, LK_TRUNC = 2, LK_BAD = 3, LK_NONE = 4 };
 
 struct alignas(16) Lds {
-	uint8_t ring[RING];
-	uint8_t inb[IN_STAGE];
-	uint64_t vis[LANES];
-	int32_t X[LANES];       // own-walk exit (-1: invalid token)
+	uint8_t ring[RING];     // output: position x at ring[x mod RING]
+	uint8_t inb[IN_STAGE];  // staged compressed bytes of the batch
+	uint32_t rec[MAXTOK];   // batch sequences: (start - s) | (output offset << 16)
+	uint32_t vis[LANES];    // positions each lane's own walk visited
+	int32_t X[LANES];       // own-walk exit (-1: malformed sequence)
 	int32_t sp[LANES];      // where the continuation stopped
-	int32_t dec[LANES];     // decoded bytes of the own walk / of the path part
-	int32_t cdec[LANES];    // decoded bytes of the continuation
-	int32_t O[LANES + 1];   // batch-relative output start of each region's sequences
+	int32_t entry[LANES];   // exact chain entry of path lanes, else -1
 	int32_t eR[LANES];      // first true sequence starting in each region
-	int32_t entry[LANES];   // exact chain entry (path lanes), else -1
+	int32_t O[LANES + 1];   // output offset of each region's first sequence
+	int32_t TB[LANES + 1];  // index of each region's first sequence
 	uint16_t J[LEVELS + 1][LANES + 1];
 	uint16_t node[LANES];
-	uint32_t done[NDONE];   // batch output bytes written (phase bitmap)
 	uint8_t link[LANES];
+	uint32_t done[NDONE];   // batch output bytes written (bitmap)
 	int32_t wsum[WAVES];
-	int32_t first_term;
-	int32_t lastp;
-	int32_t next_s;
-	int32_t total;
-	int32_t fail;
-	int32_t cutlane;  // first path lane starting at or past OUT_CAP
-	int32_t cutdone;  // a lane cut the batch inside its sequences
-	int32_t fail_dbg;
+	int32_t wsum2[WAVES];
+	int32_t first_term, lastp, next_s, total, ntok, fail, cut_idx;
 };
 
 struct Tok {
@@ -278,33 +275,71 @@ __device__ __forceinline__ Step step(const Src& S, int32_t p, int32_t n)
 	return step_slow(S, p, n);
 }
 
-// ring index of batch-relative output position rel (rel >= -HIST)
-__device__ __forceinline__ int32_t ridx(int32_t oring, int32_t rel)
+// ring index of output position o + rel; callers pass oring = o mod RING
+// and -RING < rel < RING
+__device__ __forceinline__ uint32_t ridx(int32_t oring, int32_t rel)
 {
 	int32_t i = oring + rel;
 	i += (i < 0) ? RING : 0;
 	i -= (i >= RING) ? RING : 0;
-	return i;
+	return uint32_t(i);
 }
 
-__device__ __forceinline__ u32x4 ring_ld16(const uint8_t* ring, int32_t i)
+__device__ __forceinline__ u32x4 ring_ld16(const uint8_t* ring, uint32_t i)
 {
-	return ld16u(ring, uint32_t(i), RING);
+	return ld16u(ring, i, RING);
 }
 
-__device__ __forceinline__ void ring_st(uint8_t* ring, int32_t i, u32x4 v, int32_t nb)
+__device__ __forceinline__ void ring_st(uint8_t* ring, uint32_t i, u32x4 v, int32_t nb)
 {
-	if (i + nb <= RING) {
+	if (i + uint32_t(nb) <= uint32_t(RING)) {
 		lds_store_n(ring + i, v, nb);
 	} else {
 		uint8_t t[16];
 		__builtin_memcpy(t, &v, 16);
 		for (int k = 0; k < nb; ++k) {
-			int32_t j = i + k;
-			j -= (j >= RING) ? RING : 0;
+			uint32_t j = i + k;
+			j -= (j >= uint32_t(RING)) ? uint32_t(RING) : 0u;
 			ring[j] = t[k];
 		}
 	}
+}
+
+// Next sequence start from the batch table, or parsed when the table has
+// no entry (long extensions, block end, positions past the batch).  -1:
+// malformed.
+__device__ __forceinline__ int32_t nstep(const Lds& W, const Src& S, int32_t p, int32_t n)
+{
+	(void)W;
+	return step(S, p, n).next;
+}
+
+// Workgroup exclusive prefix sums of two values (lane order).
+__device__ __forceinline__ void wg_excl_scan2(Lds& W, int32_t v0, int32_t v1, int32_t& x0,
+                                              int32_t& x1, int32_t& t0, int32_t& t1)
+{
+	const int32_t tid = int32_t(threadIdx.x);
+	const int32_t lane = tid & 63, wave = tid >> 6;
+	const int32_t i0 = wave_incl_scan(v0), i1 = wave_incl_scan(v1);
+	__syncthreads();
+	if (lane == 63) {
+		W.wsum[wave] = i0;
+		W.wsum2[wave] = i1;
+	}
+	__syncthreads();
+	int32_t b0 = 0, b1 = 0, a0 = 0, a1 = 0;
+#pragma unroll
+	for (int w = 0; w < WAVES; ++w) {
+		const int32_t y0 = W.wsum[w], y1 = W.wsum2[w];
+		b0 += (w < wave) ? y0 : 0;
+		b1 += (w < wave) ? y1 : 0;
+		a0 += y0;
+		a1 += y1;
+	}
+	x0 = b0 + i0 - v0;
+	x1 = b1 + i1 - v1;
+	t0 = a0;
+	t1 = a1;
 }
 
 // Batch output bytes [a, b) marked written (LDS bitmap, one bit per byte).
@@ -331,24 +366,72 @@ __device__ __forceinline__ bool done_check(const uint32_t* done, int32_t a, int3
 	return ok;
 }
 
-// Workgroup exclusive prefix sum (lane order); returns the total in *tot.
-__device__ __forceinline__ int32_t wg_excl_scan(Lds& W, int32_t v, int32_t* tot)
+// 16 compressed bytes at block-relative sp (staged LDS, else HBM dwords).
+__device__ __forceinline__ u32x4 lit16(const Lds& W, const Src& S, int32_t sp, int32_t n)
 {
-	const int32_t tid = int32_t(threadIdx.x);
-	const int32_t lane = tid & 63, wave = tid >> 6;
-	const int32_t inc = wave_incl_scan(v);
-	if (lane == 63)
-		W.wsum[wave] = inc;
-	__syncthreads();
-	int32_t base = 0, all = 0;
-#pragma unroll
-	for (int w = 0; w < WAVES; ++w) {
-		const int32_t x = W.wsum[w];
-		base += (w < wave) ? x : 0;
-		all += x;
+	if (sp + 16 <= S.hi)
+		return ld16u(W.inb, uint32_t(sp - S.s + S.mis), 1u << 30);
+	cg8* g = S.in + sp;
+	u32x4 v;
+	v.x = ld32u_cached(g);
+	v.y = sp + 4 < n ? ld32u_cached(g + 4) : 0u;
+	v.z = sp + 8 < n ? ld32u_cached(g + 8) : 0u;
+	v.w = sp + 12 < n ? ld32u_cached(g + 12) : 0u;
+	return v;
+}
+
+// Match with offset off < 16 (period off): its bytes repeat the off source
+// bytes before dm.  The phase-0 pattern (8 bytes when off <= 8, else 16) is
+// stored every off*floor(width/off) bytes; overlapping stores write equal
+// bytes.  Lanes li, li+cnt, ... of the cooperating group take the stores.
+__device__ __forceinline__ void pattern_fill(Lds& W, int32_t oring, int32_t dm, int32_t q,
+                                             int32_t off, int32_t ml, int32_t li, int32_t cnt)
+{
+	const u32x4 sv = ring_ld16(W.ring, ridx(oring, q));
+	u32x4 pv;
+	int32_t width, stp;
+	make_pattern(uint64_t(sv.x) | (uint64_t(sv.y) << 32), uint64_t(sv.z) | (uint64_t(sv.w) << 32),
+	             off, pv, width, stp);
+	for (int32_t k = stp * li; k < ml; k += stp * cnt) {
+		const int32_t nb = (ml - k < width) ? ml - k : width;
+		ring_st(W.ring, ridx(oring, dm + k), pv, nb);
 	}
-	*tot = all;
-	return base + inc - v;
+}
+
+// One lane copies a match of ml bytes from batch-relative q to dm
+// (lz4ada.adb:845-904, overlap-safe).
+__device__ __forceinline__ void match_copy_lane(Lds& W, int32_t oring, int32_t dm, int32_t q,
+                                                int32_t off, int32_t ml)
+{
+	if (off >= 16) {
+		for (int32_t k = 0; k < ml; k += 16) {
+			const int32_t nb = (ml - k < 16) ? ml - k : 16;
+			ring_st(W.ring, ridx(oring, dm + k), ring_ld16(W.ring, ridx(oring, q + k)), nb);
+		}
+	} else {
+		pattern_fill(W, oring, dm, q, off, ml, 0, 1);
+	}
+}
+
+// The whole wave copies one long match: steps of P = min(off rounded down
+// to 16, 1024) bytes, whose sources all precede the step.
+__device__ __forceinline__ void match_copy_wave(Lds& W, int32_t oring, int32_t dm, int32_t q,
+                                                int32_t off, int32_t ml)
+{
+	const int32_t lane = int32_t(threadIdx.x & 63u);
+	if (off >= 16) {
+		const int32_t P = (off & ~15) < 1024 ? (off & ~15) : 1024;
+		for (int32_t b = 0; b < ml; b += P) {
+			const int32_t c = b + 16 * lane;
+			if (16 * lane < P && c < ml) {
+				const int32_t nb = (ml - c < 16) ? ml - c : 16;
+				ring_st(W.ring, ridx(oring, dm + c), ring_ld16(W.ring, ridx(oring, q + c)), nb);
+			}
+			asm volatile("" ::: "memory");  // in-order LDS: next step sees these
+		}
+	} else {
+		pattern_fill(W, oring, dm, q, off, ml, lane, 64);
+	}
 }
 
 // Diagnostic build only (make stamps): per-phase s_memtime sums taken by
@@ -463,33 +546,28 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 		if (tid == 0) {
 			W.first_term = LANES;
 			W.fail = 0;
-			W.cutlane = LANES;
-			W.cutdone = 0;
-			W.fail_dbg = 0;
+			W.cut_idx = INT32_MAX;
 		}
 		__syncthreads();
 		WSTAMP(WS_STAGE);
 		WSTAMP_COUNT(WS_BATCHES, 1);
 
-		// ------------------------------------------------------ own walk
 		const int32_t bend = (n - s < BATCH_IN) ? n : s + BATCH_IN;
 		const int32_t bi = s + tid * REG;
 		const bool live = bi < bend;
-		int32_t x = -1, dsum = 0;
+		const int32_t ei = (bi + REG < bend) ? bi + REG : bend;
+
+		// ------------------------------------------------------ own walk
+		int32_t x = -1;
 		{
-			uint64_t v = 0;
+			uint32_t v = 0;
 			if (live) {
-				const int32_t ei = (bi + REG < bend) ? bi + REG : bend;
 				int32_t p = bi;
 				while (p < ei) {
-					v |= uint64_t(1) << (p - bi);
-					const Step t = step(S, p, n);
-					if (t.next < 0) {
-						p = -1;
+					v |= 1u << (p - bi);
+					p = nstep(W, S, p, n);
+					if (p < 0)
 						break;
-					}
-					dsum += t.dec;
-					p = t.next;
 				}
 				x = p;
 			}
@@ -501,15 +579,21 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 		// ------------------------------------------------------ continuation
 		{
 			uint8_t lk = LK_NONE;
-			int32_t p = x, cd = 0, tgt = TERM;
+			int32_t p = x, tgt = TERM;
 			if (live && x >= 0) {
+				int32_t kc = -1;
+				uint32_t vk = 0;
 				for (int32_t steps = 0;; ++steps) {
 					if (p >= bend) {
 						lk = LK_END;
 						break;
 					}
-					const int32_t k = (p - s) / REG;
-					if ((W.vis[k] >> (p - (s + k * REG))) & 1u) {
+					const int32_t k = (p - s) >> 5;
+					if (k != kc) {
+						kc = k;
+						vk = W.vis[k];
+					}
+					if ((vk >> ((p - s) & 31)) & 1u) {
 						lk = LK_LANE;
 						tgt = k;
 						break;
@@ -518,28 +602,23 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 						lk = LK_TRUNC;
 						break;
 					}
-					const Step t = step(S, p, n);
-					if (t.next < 0) {
+					p = nstep(W, S, p, n);
+					if (p < 0) {
 						lk = LK_BAD;
 						break;
 					}
-					cd += t.dec;
-					p = t.next;
 				}
 			} else if (live) {
-				lk = LK_BAD;  // own walk hit an invalid token
+				lk = LK_BAD;  // own walk hit a malformed sequence
 			}
 			W.X[tid] = x;
 			W.sp[tid] = p;
-			W.dec[tid] = dsum;
-			W.cdec[tid] = cd;
 			W.link[tid] = lk;
 			W.J[0][tid] = uint16_t(tgt);
 			W.entry[tid] = -1;
 			W.eR[tid] = INT32_MAX;
 			if (tid == 0) {
-				W.J[0][TERM] = TERM;
-				for (int l = 1; l <= LEVELS; ++l)
+				for (int l = 0; l <= LEVELS; ++l)
 					W.J[l][TERM] = TERM;
 			}
 			if (live && lk != LK_LANE)
@@ -556,7 +635,6 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 			const int32_t ft = W.first_term;
 			const bool chain = (tid >= ft) || (W.J[0][tid] == uint16_t(tid + 1));
 			if (__syncthreads_and(chain)) {
-				// common case: every lane up to the first terminal links to the next
 				if (tid <= ft)
 					W.entry[tid] = tid == 0 ? s : W.sp[tid - 1];
 				if (tid == 0)
@@ -584,37 +662,32 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 		}
 		__syncthreads();
 		const int32_t lastp = W.lastp;  // last lane of the path
-		WSTAMP(WS_PATH);
-		{
-			const uint8_t lk = W.link[lastp];
-			if (lk == LK_BAD || lk == LK_NONE) {
-				code = DS_RETRY;  // the chain meets a malformed sequence
-				break;
-			}
+		if (W.link[lastp] == LK_BAD || W.link[lastp] == LK_NONE) {
+			code = DS_RETRY;  // the chain meets a malformed sequence
+			break;
 		}
+		WSTAMP(WS_PATH);
 
-		// ------------------------------------------------------ region entries
-		// Re-base the work on regions: lane k copies the true sequences that
-		// start in [b_k, b_{k+1}).  Their first one is the smaller of the
-		// lane's own path entry and the first stop a path continuation made
-		// in region k.
+		// ------------------------------------------------------ regions
+		// Lane k takes the true sequences starting in its region; the first
+		// one is the smaller of its own path entry and the first stop any
+		// path continuation made in the region.
 		const int32_t nexts0 = W.sp[lastp];  // end of this batch's chain
 		{
 			const int32_t e = W.entry[tid];
 			if (e >= 0) {
-				atomicMin(&W.eR[(e - s) / REG], e);
-				const uint8_t lk = W.link[tid];
-				if (lk == LK_LANE || tid == lastp) {
+				atomicMin(&W.eR[(e - s) >> 5], e);
+				if (W.link[tid] == LK_LANE || tid == lastp) {
 					int32_t p = W.X[tid];
 					const int32_t stop = W.sp[tid];
 					int32_t lastr = -1;
 					while (p < stop) {
-						const int32_t r = (p - s) / REG;
+						const int32_t r = (p - s) >> 5;
 						if (r != lastr) {
 							atomicMin(&W.eR[r], p);
 							lastr = r;
 						}
-						p = step(S, p, n).next;
+						p = nstep(W, S, p, n);
 					}
 				}
 			}
@@ -622,172 +695,157 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 		__syncthreads();
 		const int32_t ek = W.eR[tid];
 		const int32_t pend = (bi + REG < nexts0) ? bi + REG : nexts0;
-		int32_t mydec = 0;
+		int32_t mydec = 0, myn = 0;
+		bool fail = false;
 		if (ek < pend) {
 			int32_t p = ek;
 			while (p < pend) {
-				const Step t = step(S, p, n);
-				mydec += t.dec;
+				const Tok t = parse(S, p, n);
+				if (t.next < 0) {
+					fail = true;
+					break;
+				}
+				mydec += t.L + t.ml;
+				++myn;
 				p = t.next;
 			}
 		}
-		int32_t total;
-		const int32_t O = wg_excl_scan(W, mydec, &total);
-		if (tid == 0) {
-			W.next_s = nexts0;
-			W.total = total;
+		int32_t O, TBk, total, ntot;
+		wg_excl_scan2(W, mydec, myn, O, TBk, total, ntot);
+		// records (and the batch cut: the first sequence past MAXTOK or OUT_CAP)
+		if (!fail && myn) {
+			int32_t p = ek, xo = O, idx = TBk;
+			for (int32_t j = 0; j < myn; ++j) {
+				const Tok t = parse(S, p, n);
+				if (idx >= MAXTOK || xo + t.L + t.ml > OUT_CAP) {
+					atomicMin(&W.cut_idx, idx);
+					break;
+				}
+				W.rec[idx] = uint32_t(p - s) | (uint32_t(xo) << 16);
+				xo += t.L + t.ml;
+				++idx;
+				p = t.next;
+			}
 		}
-		W.O[tid] = O;
-		if (O >= OUT_CAP && mydec > 0)
-			atomicMin(&W.cutlane, tid);
 		for (int32_t w = tid; w < NDONE; w += LANES)
 			W.done[w] = 0u;
-		if (tid == 0)
-			W.O[LANES] = total;
+		if (fail)
+			atomicOr(&W.fail, 1);
 		__syncthreads();
-		WSTAMP(WS_OFFS);
-#ifdef LZ4ADA_WG_CHECK
-		if (tid == 0) {
-			int32_t p = s, sum = 0, nt = 0;
-			while (p < nexts0) {
-				const Tok t = parse(S, p, n);
-				if (t.next < 0)
-					break;
-				sum += t.L + t.ml;
-				p = t.next;
-				++nt;
-			}
-			if (p != nexts0 || sum != total)
-				printf("[wgcheck] b=%u s=%d o=%d lastp=%d link=%d next=%d walk=%d total=%d "
-				       "walksum=%d ntok=%d fast=%d\n",
-				       b, s, o, lastp, int(W.link[lastp]), nexts0, p, total, sum, nt,
-				       int(W.first_term));
-		}
-#endif
-		if (o + (total < OUT_CAP ? total : OUT_CAP) > cap) {
-			code = DS_RETRY;  // slot overflow: exact path reports D5
+		if (W.fail) {
+			code = DS_RETRY;
 			break;
 		}
+		const int32_t cut = W.cut_idx;
+		if (cut != INT32_MAX && myn && cut >= TBk && cut < TBk + myn) {
+			// this region holds the first sequence that does not fit
+			int32_t p = ek, xo = O;
+			for (int32_t j = TBk; j < cut; ++j) {
+				const Tok t = parse(S, p, n);
+				xo += t.L + t.ml;
+				p = t.next;
+			}
+			W.next_s = p;
+			W.total = xo;
+			W.ntok = cut;
+		}
+		if (tid == 0 && cut == INT32_MAX) {
+			W.next_s = nexts0;
+			W.total = total;
+			W.ntok = ntot;
+		}
+		__syncthreads();
+		const int32_t T = W.total, nexts = W.next_s, nseq = W.ntok;
+		if (nseq == 0 || o + T > cap) {
+			code = DS_RETRY;  // a sequence larger than a batch, or a slot overflow
+			break;
+		}
+		WSTAMP(WS_OFFS);
+
+		const int32_t oring = o % RING;
 
 		// ------------------------------------------------------ copy
-		// Phase A: every lane copies the literals of its region's sequences
-		// (no dependencies) and marks those output bytes done in a bitmap.
-		// Phase B: matches, in order per lane; a match runs once every
-		// source byte it reads is marked done (bytes before the batch always
-		// are), then marks its own bytes.  A lane only waits on earlier
-		// output, so the batch always completes.
-		const int32_t oring = o % RING;
-		// stores never pass the lane's range (or the batch cap)
-		const int32_t lim = (O + mydec < OUT_CAP) ? O + mydec : OUT_CAP;
-		int32_t ntok = 0;  // sequences this lane owns in this batch (after a cut)
-		bool fail = false;
-		{
-			int32_t p = ek, xo = O;
-			bool go = (mydec > 0) && O < OUT_CAP;
-			while (go && p < pend) {
-				const Tok t = parse(S, p, n);
-				if (t.next < 0 || (t.ml && o + xo + t.L - t.off < 0)) {
-					fail = true;  // malformed, or reaches before the block (D2)
-					break;
-				}
-				if (xo + t.L + t.ml > OUT_CAP) {
-					if (xo == 0)
-						fail = true;  // one sequence larger than a batch
-					W.next_s = p;
-					W.total = xo;
-					W.cutdone = 1;
-					break;
-				}
-				for (int32_t k = 0; k < t.L; k += 16) {
-					const int32_t sp = t.lit + k;
-					u32x4 v;
-					if (sp + 16 <= S.hi) {
-						v = ld16u(W.inb, uint32_t(sp - s + S.mis), 1u << 30);
-					} else {
-						uint8_t tb[16];
-						for (int j = 0; j < 16; ++j)
-							tb[j] = (sp + j < n) ? uint8_t(S.rd(sp + j)) : 0;
-						__builtin_memcpy(&v, tb, 16);
-					}
-					const int32_t room = lim - (xo + k);
-					ring_st(W.ring, ridx(oring, xo + k), v, room < 16 ? room : 16);
-				}
-				xo += t.L + t.ml;
-				p = t.next;
-				++ntok;
-			}
-		}
-		__syncthreads();
-		// literal bytes done (a separate pass keeps the atomics off the copy)
-		{
-			int32_t p = ek, xo = O;
-			for (int32_t i = 0; i < ntok; ++i) {
-				const Tok t = parse(S, p, n);
-				if (t.L)
-					done_mark(W.done, xo, xo + t.L);
-				xo += t.L + t.ml;
-				p = t.next;
-			}
-		}
-		__syncthreads();
-		WSTAMP(WS_CP_LIT);
-		{
-			int32_t p = ek, xo = O, left = ntok;
-			int32_t iters = 0;
-			bool have = false;
+		// Rounds of LANES sequences in output order.  Literals first (no
+		// dependencies), then the match once every source byte it reads from
+		// this batch is marked done; bytes before the batch always are.
+#ifdef LZ4ADA_STAMPS
+		uint64_t cs_acc[5] = {};
+		uint64_t cs_t = __builtin_amdgcn_s_memtime();
+#endif
+		for (int32_t base = 0; base < nseq; base += LANES) {
+			const int32_t i = base + tid;
+			const bool act = i < nseq;
 			Tok t = {};
-			while (__any(left > 0)) {
+			int32_t xo = 0;
+			if (act) {
+				const uint32_t r = W.rec[i];
+				t = parse(S, s + int32_t(r & 0xffffu), n);
+				xo = int32_t(r >> 16);
+			}
+			CSTAMP(WS_CP_PARSE);
+			if (act && t.L <= LONG) {
+				for (int32_t k = 0; k < t.L; k += 16) {
+					const int32_t nb = (t.L - k < 16) ? t.L - k : 16;
+					ring_st(W.ring, ridx(oring, xo + k), lit16(W, S, t.lit + k, n), nb);
+				}
+			}
+			// long literal runs: the whole wave, one run at a time
+			for (uint64_t lm = __ballot(act && t.L > LONG); lm; lm &= lm - 1) {
+				const int k = __ffsll((long long)lm) - 1;
+				const int32_t Lk = __shfl(t.L, k), litk = __shfl(t.lit, k), xk = __shfl(xo, k);
+				for (int32_t c = 16 * (tid & 63); c < Lk; c += 1024) {
+					const int32_t nb = (Lk - c < 16) ? Lk - c : 16;
+					ring_st(W.ring, ridx(oring, xk + c), lit16(W, S, litk + c, n), nb);
+				}
+			}
+			CSTAMP(WS_CP_LIT);
+			if (act) {
+				if (t.L) {
+					asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+					done_mark(W.done, xo, xo + t.L);
+				}
+				if (t.ml && o + xo + t.L - t.off < 0)
+					fail = true;  // reference before the block start (D2)
+			}
+			CSTAMP(WS_CP_READY);
+			bool pend_m = act && t.ml && !fail;
+			int32_t iters = 0;
+			asm volatile("; MARK_MATCH_BEGIN" ::: "memory");
+			while (__any(pend_m)) {
 				if (++iters > (1 << 22)) {
 					fail = true;
 					break;
 				}
 				bool progressed = false;
-				if (left > 0) {
-					if (!have) {
-						t = parse(S, p, n);
-						have = true;
-					}
-					const int32_t dm = xo + t.L;   // match start (batch-relative)
-					const int32_t q = dm - t.off;  // match source
-					bool ready = true;
-					if (t.ml) {
-						// source bytes before the match start: [q, min(q+ml, dm))
-						const int32_t e = (q + t.ml < dm) ? q + t.ml : dm;
-						ready = done_check(W.done, q > 0 ? q : 0, e);
-					}
-					if (ready) {
-						if (t.ml) {
-							const int32_t off = t.off;
-							if (off >= 16) {
-								for (int32_t k = 0; k < t.ml; k += 16) {
-									const int32_t nb = (t.ml - k < 16) ? t.ml - k : 16;
-									const u32x4 v = ring_ld16(W.ring, ridx(oring, q + k));
-									ring_st(W.ring, ridx(oring, dm + k), v, nb);
-								}
-							} else {
-								// period off < 16: the 16-byte pattern of phase 0,
-								// stored every off*floor(16/off) bytes
-								const u32x4 sv = ring_ld16(W.ring, ridx(oring, q));
-								unsigned __int128 x;
-								__builtin_memcpy(&x, &sv, 16);
-								x &= (((unsigned __int128)1) << (8 * off)) - 1;
-								for (int32_t w = off; w < 16; w <<= 1)
-									x |= x << (8 * w);
-								u32x4 pv;
-								__builtin_memcpy(&pv, &x, 16);
-								const int32_t stp = off * (16 / off);
-								for (int32_t k = 0; k < t.ml; k += stp) {
-									const int32_t nb = (t.ml - k < 16) ? t.ml - k : 16;
-									ring_st(W.ring, ridx(oring, dm + k), pv, nb);
-								}
-							}
-							asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-							done_mark(W.done, dm, dm + t.ml);
-						}
-						xo += t.L + t.ml;
-						p = t.next;
-						have = false;
-						--left;
+				const int32_t dm = xo + t.L;
+				const int32_t q = dm - t.off;
+				bool ready = false;
+				if (pend_m) {
+					const int32_t e = (q + t.ml < dm) ? q + t.ml : dm;
+#ifdef LZ4ADA_WG_EXP_NODEPS
+					ready = true;
+					(void)e;
+#else
+					ready = done_check(W.done, q > 0 ? q : 0, e);
+#endif
+				}
+				if (pend_m && ready && t.ml <= LONG) {
+					match_copy_lane(W, oring, dm, q, t.off, t.ml);
+					asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+					done_mark(W.done, dm, dm + t.ml);
+					pend_m = false;
+					progressed = true;
+				}
+				// long matches: the whole wave, one at a time
+				for (uint64_t lm = __ballot(pend_m && ready && t.ml > LONG); lm; lm &= lm - 1) {
+					const int k = __ffsll((long long)lm) - 1;
+					const int32_t dk = __shfl(dm, k), qk = __shfl(q, k);
+					const int32_t ok = __shfl(t.off, k), mk = __shfl(t.ml, k);
+					match_copy_wave(W, oring, dk, qk, ok, mk);
+					if ((tid & 63) == k) {
+						asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+						done_mark(W.done, dk, dk + mk);
+						pend_m = false;
 						progressed = true;
 					}
 				}
@@ -795,9 +853,18 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 					__builtin_amdgcn_s_sleep(1);
 			}
 #ifdef LZ4ADA_STAMPS
-			atomicMax(&W.fail_dbg, iters);
+			WSTAMP_COUNT(WS_ITERS, iters);
 #endif
+			asm volatile("; MARK_MATCH_END" ::: "memory");
+			CSTAMP(WS_CP_MATCH);
+			// no barrier: a wave moves on to its next sequences at once (they
+			// only ever wait on lower-numbered ones, which always complete)
+			CSTAMP(WS_CP_REST);
 		}
+#ifdef LZ4ADA_STAMPS
+		for (int k = 0; k < 5; ++k)
+			ws_acc[WS_CP_PARSE + k] += cs_acc[k];
+#endif
 		if (fail)
 			atomicOr(&W.fail, 1);
 		__syncthreads();
@@ -806,16 +873,7 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 			break;
 		}
 		WSTAMP(WS_COPY);
-		WSTAMP_COUNT(WS_CUTS, W.cutdone || W.cutlane < LANES);
-#ifdef LZ4ADA_STAMPS
-		WSTAMP_COUNT(WS_ITERS, W.fail_dbg);
-#endif
-		int32_t T = W.total, nexts = W.next_s;
-		if (!W.cutdone && W.cutlane < LANES) {
-			// the batch is full exactly at a region boundary
-			T = W.O[W.cutlane];
-			nexts = W.eR[W.cutlane];
-		}
+		WSTAMP_COUNT(WS_CUTS, nexts != nexts0);
 
 		// ------------------------------------------------------ flush
 		{
@@ -832,12 +890,9 @@ __global__ __launch_bounds__(LANES) void k_decode_wg(const uint8_t* __restrict__
 			for (int32_t i = h + nv * 16 + tid; i < T; i += LANES)
 				dst[i] = W.ring[ridx(oring, i)];
 		}
+		// later batches read old output back from HBM (sources > 32 KiB back)
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__syncthreads();
-#ifdef LZ4ADA_WG_CHECK
-		if (tid == 0 && b == 0)
-			printf("[wgbatch] s=%d o=%d T=%d next=%d lastp=%d ft=%d\n", s, o, T, nexts, lastp,
-			       W.first_term);
-#endif
 		WSTAMP(WS_FLUSH);
 		o += T;
 		s = nexts;

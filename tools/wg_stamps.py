@@ -18,7 +18,7 @@ import torch  # noqa: E402
 
 PH = ["stage", "walk", "cont", "path", "offsets", "copy", "flush"]
 CNT = ["batches", "slowpath", "copy_iters", "cuts"]
-CP = ["cp_parse", "cp_ready", "cp_lit", "cp_match", "cp_rest"]
+CP = ["cp_parse", "cp_marklit", "cp_lit", "cp_match", "cp_barrier"]
 
 
 def main():
@@ -57,7 +57,7 @@ def main():
     for i, name in enumerate(CNT):
         print(f"  {name:10s} {v[7 + i] / nbat:10.2f} per batch")
     for i, name in enumerate(CP):
-        print(f"  {name:10s} {v[11 + i] / nbat:10.0f} cyc/batch (wave 0, inside copy)")
+        print(f"  {name:10s} {v[11 + i] / nbat:10.0f} cyc/batch (wave 0, copy rounds)")
 
 
 if __name__ == "__main__":
