@@ -1121,6 +1121,19 @@ int lz4ada_launch_decode(const void* d_frame, uint64_t frame_len, const lz4ada_b
 	});
 }
 
+int lz4ada_launch_decode_variant(const void* d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc* d_descs, int64_t nblocks, void* d_out,
+                                 lz4ada_block_status* d_status, int variant, void* stream)
+{
+	return guarded(nullptr, [&] {
+		if (variant < 0 || variant > 2)
+			raise(LZ4ADA_ASSERTION_ERROR, "unknown decoder variant");
+		HIP_OK(launch_decode_variant(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
+		                             uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,
+		                             variant, static_cast<hipStream_t>(stream)));
+	});
+}
+
 int lz4ada_launch_decode_wg(const void* d_frame, uint64_t frame_len,
                             const lz4ada_block_desc* d_descs, int64_t nblocks, void* d_out,
                             lz4ada_block_status* d_status, void* stream)

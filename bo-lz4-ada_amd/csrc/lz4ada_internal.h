@@ -51,9 +51,16 @@ struct SerialState {
 // ---- launchers (lz4ada_kernels.hip) ----
 // All launch on `stream` and never synchronise.
 
-// Bulk independent-block decode: k_decode_blocks (one wavefront per
-// block).  LZ4ADA_DECODER=wg runs k_decode_wg (workgroup per block) first
-// and k_decode_blocks only for the blocks it declined.
+// Bulk independent-block decoders (LZ4ADA_DECODE_* in lz4ada_hip.h).
+enum DecVariant : int { DEC_PC = 0, DEC_WAVE = 1, DEC_WG = 2 };
+
+hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                 uint8_t* d_out, lz4ada_block_status* d_status, int variant,
+                                 hipStream_t stream);
+
+// The default decoder: k_decode_pc (producer + consumer wave per block);
+// LZ4ADA_DECODER=wave / wg select the others.
 hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                 uint8_t* d_out, lz4ada_block_status* d_status,

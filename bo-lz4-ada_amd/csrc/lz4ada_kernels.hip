@@ -292,6 +292,8 @@ __device__ unsigned long long g_stamps[SP_N];
 		st_t = _t;                                                         \
 	} while (0)
 #define STAMP_COUNT(ph, v) (st_acc[ph] += uint64_t(v))
+#define STAMP_PARAM , uint64_t(&st_acc)[SP_N], uint64_t& st_t
+#define STAMP_ARGS , st_acc, st_t
 #define STAMP_FLUSH()                                                              \
 	do {                                                                       \
 		if (lane_id() == 0)                                                \
@@ -302,6 +304,8 @@ __device__ unsigned long long g_stamps[SP_N];
 #define STAMP_DECL
 #define STAMP(ph)
 #define STAMP_COUNT(ph, v)
+#define STAMP_PARAM
+#define STAMP_ARGS
 #define STAMP_FLUSH()
 #endif
 
@@ -373,6 +377,14 @@ __device__ void wave_copy(g8* __restrict__ dst, cg8* __restrict__ src, int64_t n
 // One token at block-relative s, wave-cooperative, global -> global.
 // Handles every shape, including the malformed ones (exact statuses).
 // Returns false with st filled on error; advances s and o.
+// Every global store and LDS op of this wave done (one-token path; the
+// path is run by a single wave, also inside the two-wave decoder, so it
+// must not use a workgroup barrier).
+__device__ __forceinline__ void wave_mem_fence()
+{
+	asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 __device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
                           int64_t cap, int64_t& s, int64_t& o, lz4ada_block_status& st)
 {
@@ -410,7 +422,7 @@ __device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
 			return false;
 		}
 		s = p;
-		__syncthreads();
+		wave_mem_fence();
 		return true;
 	}
 	if (p + 1 >= n) {
@@ -443,7 +455,7 @@ __device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
 		st.err_out_pos = o;
 		return false;
 	}
-	__syncthreads();  // literals above are visible to every lane
+	wave_mem_fence();  // literals above are visible to every lane
 	if (off >= ml) {
 		wave_copy(ob + o, ob + q0, ml);
 	} else {
@@ -461,7 +473,7 @@ __device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
 	}
 	o += ml;
 	s = p;
-	__syncthreads();
+	wave_mem_fence();
 	return true;
 }
 
@@ -662,7 +674,8 @@ __device__ __forceinline__ u32x4 load_chunk(cg8* in, uintptr_t lim_addr, int32_t
 	return v;
 }
 
-__device__ __forceinline__ void stage_to(DecLds& L, cg8* in, uintptr_t lim_addr, int32_t mis,
+template <class LdsT>
+__device__ __forceinline__ void stage_to(LdsT& L, cg8* in, uintptr_t lim_addr, int32_t mis,
                                          int32_t& hi, u32x4& pf0, u32x4& pf1, int32_t lo,
                                          int32_t need)
 {
@@ -1064,6 +1077,438 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 	}
 }
 
+// ------------------------------------------- producer/consumer decoder
+// k_decode_pc: the per-wave decoder split over two waves of one workgroup
+// per block.  Wave 0 (producer) stages the compressed stream and parses
+// windows into batches of sequence records; wave 1 (consumer) copies the
+// previous batch (literals, dependency-ordered matches, 16-byte flush to
+// HBM).  The two run in lockstep, one barrier per step, with the records
+// double-buffered, so a step costs max(parse, copy) instead of their sum,
+// and each CU holds 16 waves instead of 8.  Anything unusual goes through
+// the same one-token path, run by the producer once every batch is out.
+
+constexpr int PC_BIG = BIG;            // longer sequences take the one-token path
+constexpr int PC_SPAN = SPAN;          // compressed bytes a batch may span
+constexpr int PC_STAGE_AHEAD = STAGE_AHEAD;
+// The ring also holds the batch the consumer is copying: the producer ends
+// its batch early (or waits a step) rather than stage over those bytes.
+
+struct alignas(16) PcLds {
+	uint16_t J[6][WIN];
+	uint8_t inb[INB + MIRROR];
+	uint8_t outb[OUTB + 32];
+	int32_t r_tstart[2][MAXTOK];
+	int32_t r_L[2][MAXTOK];
+	int32_t r_lit[2][MAXTOK];
+	int32_t r_off[2][MAXTOK];
+	int32_t r_ml[2][MAXTOK];
+	int32_t m_nb[2], m_blen[2], m_o[2], m_bcomp0[2];
+	int32_t flags;  // bit 0: producer finished, bit 1: one-token step pending
+};
+
+// Consumer: copy batch `c` (records, output at o) into outb and flush it.
+__device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* __restrict__ ob STAMP_PARAM)
+{
+	const int lane = int(lane_id());
+	const int32_t nb = L.m_nb[c], blen = L.m_blen[c], o = L.m_o[c];
+	const bool tl = lane < nb;
+	const int32_t ts = tl ? L.r_tstart[c][lane] : 0;
+	const int32_t tL = tl ? L.r_L[c][lane] : 0;
+	const int32_t tlit = tl ? L.r_lit[c][lane] : 0;
+	const int32_t toff = tl ? L.r_off[c][lane] : 1;
+	const int32_t tml = tl ? L.r_ml[c][lane] : 0;
+	const int32_t d0 = ts + tL;        // batch-relative
+	const int32_t q0 = o + d0 - toff;  // block-relative source
+	u32x4 pv0 = {0, 0, 0, 0}, pv1 = {0, 0, 0, 0};
+	const bool pre0 = tl && tml > 0 && toff >= 16 && q0 + 16 <= o;
+	const bool pre1 = pre0 && tml > 16 && q0 + 32 <= o;
+	if (pre0)
+		__builtin_memcpy(&pv0, (const uint8_t*)(ob + q0), 16);
+	if (pre1)
+		__builtin_memcpy(&pv1, (const uint8_t*)(ob + q0 + 16), 16);
+	constexpr int32_t LONG = 48;
+	if (tL <= LONG) {
+		for (int32_t i = 0; i < tL; i += 16) {
+			u32x4 v;
+			__builtin_memcpy(&v, &L.inb[(tlit + i + mis) & INB_MASK], 16);
+			lds_store_n(&L.outb[ts + i], v, tL - i);
+		}
+	}
+	for (uint64_t lm = __ballot(tl && tL > LONG); lm; lm &= lm - 1) {
+		const int k = __ffsll((long long)lm) - 1;
+		const int32_t Lk = __shfl(tL, k), litk = __shfl(tlit, k), tsk = __shfl(ts, k);
+		for (int32_t i = 16 * lane; i < Lk; i += 1024) {
+			u32x4 v;
+			__builtin_memcpy(&v, &L.inb[(litk + i + mis) & INB_MASK], 16);
+			lds_store_n(&L.outb[tsk + i], v, Lk - i);
+		}
+	}
+	wave_lds_fence();
+	STAMP(SP_LIT);
+	const int32_t sb = (q0 + tml < o + d0 ? q0 + tml : o + d0) - o;
+	const int32_t sa = (q0 - o > 0) ? q0 - o : 0;
+	const bool inbatch = tl && tml > 0 && sb > 0;
+	uint64_t dep = 0;
+	if (__ballot(inbatch)) {
+		const int32_t ka = owner_of(ts, nb, inbatch ? sa : 0);
+		const int32_t kb = owner_of(ts, nb, inbatch ? sb - 1 : 0);
+		const int32_t d0_ka = __shfl(d0, ka), ml_ka = __shfl(tml, ka);
+		const int32_t d0_kb = __shfl(d0, kb), ml_kb = __shfl(tml, kb);
+		if (inbatch) {
+			if (kb > ka + 1)
+				dep = ((1ull << kb) - 1) & ~((2ull << ka) - 1);
+			if (ml_ka > 0 && d0_ka < sb && d0_ka + ml_ka > sa)
+				dep |= 1ull << ka;
+			if (kb != ka && ml_kb > 0 && d0_kb < sb)
+				dep |= 1ull << kb;
+			dep &= (1ull << lane) - 1;
+		}
+	}
+	bool pend = tl && tml > 0;
+	for (int guard = 0;; ++guard) {
+		const uint64_t pm = __ballot(pend);
+		if (!pm)
+			break;
+		const bool ready = pend && (!(pm & dep) || guard > MAXTOK);
+		if (ready) {
+			if (toff >= 16) {
+				for (int32_t i = 0; i < tml; i += 16) {
+					const int32_t sp = q0 + i;
+					const int32_t nn = tml - i < 16 ? tml - i : 16;
+					u32x4 v;
+					if (i == 0 && pre0) {
+						v = pv0;
+					} else if (i == 16 && pre1) {
+						v = pv1;
+					} else if (sp + 16 <= o) {
+						__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
+					} else if (sp >= o) {
+						__builtin_memcpy(&v, &L.outb[sp - o], 16);
+					} else {
+						uint8_t t[16];
+						for (int k = 0; k < 16; ++k)
+							t[k] = (sp + k < o) ? ob[sp + k] : L.outb[sp + k - o];
+						__builtin_memcpy(&v, t, 16);
+					}
+					lds_store_n(&L.outb[d0 + i], v, nn);
+				}
+			} else {
+				int32_t r = 0;
+				for (int32_t k = 0; k < tml; ++k) {
+					const int32_t sp = q0 + r;
+					L.outb[d0 + k] = (sp < o) ? ob[sp] : L.outb[sp - o];
+					if (++r == toff)
+						r = 0;
+				}
+			}
+		}
+		pend = pend && !ready;
+		wave_lds_fence();
+		STAMP_COUNT(SP_ROUNDS, 1);
+	}
+	STAMP(SP_MATCH);
+	{
+		g8* dst = ob + o;
+		const int32_t head = int32_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
+		const int32_t h = head < blen ? head : blen;
+		if (lane < h)
+			dst[lane] = L.outb[lane];
+		const int32_t nv = (blen - h) / 16;
+		for (int32_t i = lane; i < nv; i += 64) {
+			u32x4 v;
+			__builtin_memcpy(&v, &L.outb[h + 16 * i], 16);
+			*reinterpret_cast<GLOBAL u32x4*>(dst + h + 16 * i) = v;
+		}
+		for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)
+			dst[i] = L.outb[i];
+	}
+	// later batches (either wave) read this output back from HBM
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	STAMP(SP_FLUSH);
+	STAMP_COUNT(SP_BATCHES, 1);
+}
+
+__global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ frame,
+                                                    uint64_t frame_len,
+                                                    const lz4ada_block_desc* __restrict__ desc,
+                                                    uint32_t nblocks, uint8_t* __restrict__ out,
+                                                    lz4ada_block_status* __restrict__ status,
+                                                    int retry_only)
+{
+	__shared__ PcLds L;
+
+	const uint32_t b = blockIdx.x;
+	if (b >= nblocks)
+		return;
+	if (retry_only && status[b].code != DS_RETRY)
+		return;
+	const int wave = int(threadIdx.x >> 6);
+	const int lane = int(lane_id());
+	const lz4ada_block_desc d = desc[b];
+	cg8* __restrict__ in = gptr(frame) + d.in_off;
+	g8* __restrict__ ob = gptr(out) + d.out_off;
+	const int32_t n = int32_t(d.in_len);
+	const int32_t cap = int32_t(d.out_cap);
+
+	lz4ada_block_status st;
+	st.code = DS_OK;
+	st.aux = 0;
+	st.detail = 0;
+	st.err_out_pos = 0;
+	st.out_len = 0;
+
+	if (d.flags & LZ4ADA_BLOCK_STORED) {
+		if (wave == 0) {
+			if (n > cap) {
+				st.code = DS_OUT_OVERFLOW;
+			} else {
+				wave_copy(ob, in, n);
+				st.out_len = uint32_t(n);
+			}
+			if (lane == 0) {
+				status[b].code = st.code;
+				status[b].aux = 0;
+				status[b].detail = 0;
+				status[b].err_out_pos = 0;
+				status[b].out_len = st.out_len;
+			}
+		}
+		return;
+	}
+
+	const uintptr_t lim_addr = reinterpret_cast<uintptr_t>(frame) + frame_len;
+	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+	// producer state (wave 0)
+	int32_t s = 0, o = 0, hi = -mis;
+	u32x4 pf0 = {0, 0, 0, 0}, pf1 = {0, 0, 0, 0};
+	if (wave == 0) {
+		pf0 = load_chunk(in, lim_addr, hi);
+		pf1 = load_chunk(in, lim_addr, hi + 1024);
+	}
+	bool ok = true;
+	bool pdone = (n == 0);
+	bool pone = false;  // one-token step pending
+	if (threadIdx.x == 0) {
+		L.m_nb[0] = L.m_nb[1] = 0;
+		L.flags = pdone ? 1 : 0;
+	}
+	__syncthreads();
+	STAMP_DECL;
+	int slot = 0;  // the producer fills `slot`, the consumer drains slot ^ 1
+	for (int32_t step = 0;; ++step) {
+		if (wave == 0) {
+			// ------------------------------------------------ producer
+			if (!pdone && !pone) {
+				const int c = slot ^ 1;
+				const int32_t keep = L.m_nb[c] > 0 ? L.m_bcomp0[c] : INT32_MAX;
+				int32_t nb = 0, blen = 0, bcomp0 = s;
+				for (int32_t iter = 0;; ++iter) {
+					if (iter > 4 * n + 64) {
+						st.code = DS_INTERNAL;
+						ok = false;
+						pdone = true;
+						break;
+					}
+					bool stop = false, end_block = false, force_flush = false;
+					if (keep != INT32_MAX && s + PC_STAGE_AHEAD + 1024 + MIRROR - keep > INB) {
+						// staging further would overwrite the consumer's batch
+						if (lane == 0) {
+							L.m_nb[slot] = nb;
+							L.m_blen[slot] = blen;
+							L.m_o[slot] = o;
+							L.m_bcomp0[slot] = bcomp0;
+						}
+						o += blen;
+						break;
+					}
+					{
+						int32_t lo = nb ? bcomp0 : s;
+						lo = keep < lo ? keep : lo;
+						stage_to(L, in, lim_addr, mis, hi, pf0, pf1, lo, s + PC_STAGE_AHEAD);
+						STAMP(SP_STAGE);
+						STAMP_COUNT(SP_WINDOWS, 1);
+					}
+					const uint32_t peek =
+					    uint32_t(uni(int32_t(lds_u16(L.inb + ((s + mis) & INB_MASK)))));
+					if ((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) {
+						Cand t = {};
+						bool okp = parse_serial(L.inb, mis, s, n, hi, t);
+						const int32_t klen = t.L + t.ml;
+						const int32_t d0 = o + blen + t.L;
+						okp = okp && nb < MAXTOK && klen <= PC_BIG && blen + klen <= OUTB &&
+						      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
+						      (t.off >= 16 || t.ml <= 64);
+						if (okp) {
+							if (lane == 0) {
+								L.r_tstart[slot][nb] = blen;
+								L.r_L[slot][nb] = t.L;
+								L.r_lit[slot][nb] = t.lit;
+								L.r_off[slot][nb] = t.off;
+								L.r_ml[slot][nb] = t.ml;
+							}
+							if (nb == 0)
+								bcomp0 = s;
+							++nb;
+							blen += klen;
+							STAMP_COUNT(SP_TOKENS, 1);
+							end_block = (t.kind == TK_LAST || t.next >= n);
+							s = t.next;
+						} else if (nb == 0) {
+							stop = true;
+						} else {
+							force_flush = true;
+						}
+					} else {
+#pragma unroll
+						for (int q = 0; q < WIN / 64; ++q) {
+							const int k = 64 * q + lane;
+							const Cand t = parse_cand(L.inb, mis, s + k, n);
+							const int32_t rel = t.next - s;
+							L.J[0][k] = uint16_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0xffff);
+						}
+						wave_lds_fence();
+						STAMP(SP_CAND);
+#pragma unroll
+						for (int r = 0; r < 5; ++r) {
+							uint32_t a[WIN / 64];
+#pragma unroll
+							for (int q = 0; q < WIN / 64; ++q)
+								a[q] = L.J[r][64 * q + lane];
+#pragma unroll
+							for (int q = 0; q < WIN / 64; ++q)
+								a[q] = a[q] < WIN ? L.J[r][a[q]] : 0xffffu;
+#pragma unroll
+							for (int q = 0; q < WIN / 64; ++q)
+								L.J[r + 1][64 * q + lane] = uint16_t(a[q]);
+							wave_lds_fence();
+						}
+						STAMP(SP_DOUBLE);
+						uint32_t cj = 0;
+#pragma unroll
+						for (int r = 0; r < 6; ++r) {
+							const uint32_t g = cj < WIN ? L.J[r][cj] : 0xffffu;
+							if ((lane >> r) & 1)
+								cj = g;
+						}
+						const bool inwin = cj < WIN;
+						const Cand tk = parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
+						const int32_t kL = tk.L, klit = tk.lit, koff = tk.off, kml = tk.ml;
+						const int32_t knext = tk.next, kkind = tk.kind;
+						const bool good = inwin && (kkind == TK_NORMAL || kkind == TK_LAST);
+						const int32_t klen = kL + kml;
+						const int32_t incl = wave_incl_scan(good ? klen : 0);
+						const int32_t tstart = blen + incl - klen;
+						const int32_t d0 = o + tstart + kL;
+						const bool fits = good && lane < MAXTOK - nb && klen <= PC_BIG &&
+						                  blen + incl <= OUTB && o + blen + incl <= cap &&
+						                  (kkind != TK_NORMAL || d0 - koff >= 0) &&
+						                  (koff >= 16 || kml <= 64);
+						const uint64_t badm = __ballot(!fits);
+						const int cnt = badm ? (__ffsll((long long)badm) - 1) : 64;
+						const int32_t cnext = cnt > 0 ? __shfl(knext, cnt - 1) : s;
+						const int32_t ckind_last = cnt > 0 ? __shfl(kkind, cnt - 1) : TK_NORMAL;
+						if (lane < cnt) {
+							L.r_tstart[slot][nb + lane] = tstart;
+							L.r_L[slot][nb + lane] = kL;
+							L.r_lit[slot][nb + lane] = klit;
+							L.r_off[slot][nb + lane] = koff;
+							L.r_ml[slot][nb + lane] = kml;
+						}
+						STAMP_COUNT(SP_TOKENS, cnt);
+						const bool was_empty = (nb == 0);
+						if (was_empty && cnt > 0)
+							bcomp0 = s;
+						nb += cnt;
+						blen += cnt > 0 ? __shfl(incl, cnt - 1) : 0;
+						if (cnt > 0 && ckind_last == TK_LAST) {
+							end_block = true;
+							s = n;
+						} else if (cnt > 0 && cnext >= n) {
+							end_block = true;  // block ends right after a match (lz4ada.adb:780)
+							s = cnext;
+						} else if (cnt > 0) {
+							s = cnext;
+						} else if (was_empty) {
+							stop = true;
+						} else {
+							force_flush = true;
+						}
+					}
+					wave_lds_fence();
+					STAMP(SP_SELECT);
+					const bool flush = end_block || stop || force_flush ||
+					                   nb > MAXTOK - WTOK / 2 || blen > OUTB - PC_BIG ||
+					                   (s - bcomp0) >= PC_SPAN;
+					if (flush) {
+						if (lane == 0) {
+							L.m_nb[slot] = nb;
+							L.m_blen[slot] = blen;
+							L.m_o[slot] = o;
+							L.m_bcomp0[slot] = bcomp0;
+						}
+						o += blen;
+						if (end_block)
+							pdone = true;
+						if (stop)
+							pone = true;
+						break;
+					}
+				}
+			}
+		} else {
+			// ------------------------------------------------ consumer
+			const int c = slot ^ 1;
+			if (L.m_nb[c] > 0) {
+				pc_copy_batch(L, c, mis, ob STAMP_ARGS);
+				wave_lds_fence();
+				if (lane == 0)
+					L.m_nb[c] = 0;
+			}
+		}
+		__syncthreads();
+		if (threadIdx.x == 0)
+			L.flags = (pdone ? 1 : 0) | (pone ? 2 : 0);
+		__syncthreads();
+		int fl = L.flags;
+		const bool full = L.m_nb[0] > 0 || L.m_nb[1] > 0;
+		if ((fl & 2) && !full) {
+			// every batch is in HBM: the producer takes the one-token path
+			if (wave == 0) {
+				int64_t s64 = s, o64 = o;
+				if (!one_token(in, n, ob, cap, s64, o64, st)) {
+					ok = false;
+					pdone = true;
+				} else {
+					s = int32_t(s64);
+					o = int32_t(o64);
+					if (s >= n)
+						pdone = true;
+				}
+				pone = false;
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				STAMP(SP_ONE);
+			}
+			__syncthreads();
+			if (threadIdx.x == 0)
+				L.flags = (pdone ? 1 : 0);
+			__syncthreads();
+			fl = L.flags;
+		}
+		if ((fl & 1) && !full)
+			break;
+		slot ^= 1;
+	}
+	STAMP_FLUSH();
+
+	if (threadIdx.x == 0) {
+		status[b].code = ok ? int32_t(DS_OK) : st.code;
+		status[b].aux = st.aux;
+		status[b].detail = st.detail;
+		status[b].err_out_pos = st.err_out_pos;
+		status[b].out_len = uint32_t(o);
+	}
+}
+
 // Gather variable-length slots into a contiguous buffer.
 __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ src,
                                                   const lz4ada_block_desc* __restrict__ desc,
@@ -1301,28 +1746,47 @@ extern "C" int lz4ada_debug_stamps(unsigned long long* out, int reset)
 }
 #endif
 
-hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
-                                const lz4ada_block_desc* d_desc, uint32_t nblocks,
-                                uint8_t* d_out, lz4ada_block_status* d_status,
-                                hipStream_t stream)
+hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                 uint8_t* d_out, lz4ada_block_status* d_status, int variant,
+                                 hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	// LZ4ADA_DECODER=wg: workgroup decoder first (experimental; the
-	// per-wave decoder is faster on every content class measured so far)
-	static const int wave_only = [] {
-		const char* e = getenv("LZ4ADA_DECODER");
-		return (e && e[0] == 'w' && e[1] == 'g') ? 0 : 1;
-	}();
-	if (!wave_only) {
+	if (variant == DEC_PC) {
+		hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
+		                   d_desc, nblocks, d_out, d_status, 0);
+		return hipGetLastError();
+	}
+	if (variant == DEC_WG) {
 		const hipError_t err = launch_decode_wg(d_frame, frame_len, d_desc, nblocks, d_out,
 		                                        d_status, stream);
 		if (err != hipSuccess)
 			return err;
 	}
 	hipLaunchKernelGGL(k_decode_blocks, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
-	                   d_desc, nblocks, d_out, d_status, wave_only ? 0 : 1);
+	                   d_desc, nblocks, d_out, d_status, variant == DEC_WG ? 1 : 0);
 	return hipGetLastError();
+}
+
+hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
+                                const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                uint8_t* d_out, lz4ada_block_status* d_status,
+                                hipStream_t stream)
+{
+	// Default: the two-wave producer/consumer decoder.  LZ4ADA_DECODER=wave
+	// selects the one-wave decoder, LZ4ADA_DECODER=wg the experimental
+	// workgroup decoder (one-wave decoder for the blocks it declines).
+	static const int variant = [] {
+		const char* e = getenv("LZ4ADA_DECODER");
+		if (e && e[0] == 'w' && e[1] == 'g')
+			return int(DEC_WG);
+		if (e && e[0] == 'w')
+			return int(DEC_WAVE);
+		return int(DEC_PC);
+	}();
+	return launch_decode_variant(d_frame, frame_len, d_desc, nblocks, d_out, d_status, variant,
+	                             stream);
 }
 
 hipError_t launch_block_checksums(const uint8_t* d_frame, const lz4ada_block_desc* d_desc,

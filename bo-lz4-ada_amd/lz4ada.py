@@ -183,6 +183,8 @@ _sig = {
     "lz4ada_decode_blocks_device": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp],
                                     ctypes.c_int),
     "lz4ada_launch_decode": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp], ctypes.c_int),
+    "lz4ada_launch_decode_variant": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, ctypes.c_int, _vp],
+                                     ctypes.c_int),
     "lz4ada_launch_decode_wg": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lz4ada_launch_block_checksums": ([_vp, _vp, _i64, _vp, _vp], ctypes.c_int),
     "lz4ada_output_checksums_device": ([_vp, _vp, _vp, _i64, _vp, _vp], ctypes.c_int),
@@ -373,6 +375,16 @@ def decode_blocks_device(d_frame: int, frame_len: int, d_descs: int, nblocks: in
 def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=0):
     _check(_lib.lz4ada_launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status,
                                      stream), _thread_error())
+
+
+DECODE_PC, DECODE_WAVE, DECODE_WG = 0, 1, 2
+
+
+def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,
+                          stream=0):
+    """One of the bulk decoders (DECODE_PC default, DECODE_WAVE, DECODE_WG)."""
+    _check(_lib.lz4ada_launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out,
+                                             d_status, variant, stream), _thread_error())
 
 
 def launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=0):

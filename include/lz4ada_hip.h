@@ -207,6 +207,16 @@ int lz4ada_decode_blocks_device(const void *d_frame, uint64_t frame_len,
 int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
                          const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                          lz4ada_block_status *d_status, void *stream);
+/* Decoder variants of the bulk path: the default two-wave
+ * producer/consumer decoder, the one-wave decoder, and the experimental
+ * workgroup decoder followed by the one-wave decoder for declined blocks. */
+#define LZ4ADA_DECODE_PC 0
+#define LZ4ADA_DECODE_WAVE 1
+#define LZ4ADA_DECODE_WG 2
+int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
+                                 lz4ada_block_status *d_status, int variant, void *stream);
+
 /* The workgroup-per-block decoder alone: blocks it declines (malformed
  * data, oversize sequences) keep status code 10 (retry) and are not
  * decoded; lz4ada_launch_decode runs it and then redoes those blocks. */

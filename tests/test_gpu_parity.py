@@ -228,10 +228,11 @@ def test_device_resident_blocks():
 
 # ------------------------------------------- bench-sized blocks (regression)
 
+@pytest.mark.parametrize("variant", ["pc", "wave", "wg"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
-def test_bench_blocks_exact(kind):
+def test_bench_blocks_exact(kind, variant):
     """The bench's own unique 4 MiB blocks (seed 0x4C5A3441 + i) decode
-    byte-exactly through the device-resident path."""
+    byte-exactly through every bulk decoder."""
     torch = pytest.importorskip("torch")
     seeds = [0x4C5A3441 + i for i in range(16)]
     bmax = 4 << 20
@@ -245,9 +246,11 @@ def test_bench_blocks_exact(kind):
     d_desc = torch.frombuffer(bytearray(bytes(descs)[:nb * 32]), dtype=torch.uint8).to(dev)
     d_out = torch.zeros(nb * bmax, dtype=torch.uint8, device=dev)
     d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
-    lz4ada.decode_blocks_device(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
-                                d_out.data_ptr(), d_st.data_ptr(),
-                                torch.cuda.current_stream().cuda_stream)
+    sh = torch.cuda.current_stream().cuda_stream
+    lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), nb, d_st.data_ptr(), sh)
+    v = {"pc": lz4ada.DECODE_PC, "wave": lz4ada.DECODE_WAVE, "wg": lz4ada.DECODE_WG}[variant]
+    lz4ada.launch_decode_variant(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
+                                 d_out.data_ptr(), d_st.data_ptr(), v, sh)
     torch.cuda.synchronize()
     st = (lz4ada.BlockStatus * nb).from_buffer_copy(d_st.cpu().numpy().tobytes())
     out = d_out.cpu().numpy().tobytes()
