@@ -280,7 +280,7 @@ enum TokKind : int { TK_NORMAL = 0, TK_LAST = 1, TK_COMPLEX = 2, TK_ERR = 3 };
 // s_memtime sums of k_decode_blocks, read back by tools/stamps.py.  The
 // product library is built without LZ4ADA_STAMPS and executes no stamp.
 enum StampPhase { SP_STAGE, SP_CAND, SP_DOUBLE, SP_SELECT, SP_LIT, SP_MATCH, SP_FLUSH, SP_ONE,
-	          SP_BATCHES, SP_WINDOWS, SP_TOKENS, SP_ROUNDS, SP_N };
+	          SP_WAIT, SP_DEP, SP_BATCHES, SP_WINDOWS, SP_TOKENS, SP_ROUNDS, SP_N };
 #ifdef LZ4ADA_STAMPS
 __device__ unsigned long long g_stamps[SP_N];
 #define STAMP_DECL uint64_t st_acc[SP_N] = {}; uint64_t st_t = __builtin_amdgcn_s_memtime()
@@ -1104,6 +1104,8 @@ struct alignas(16) PcLds {
 	int32_t r_ml[2][MAXTOK];
 	int32_t m_nb[2], m_blen[2], m_o[2], m_bcomp0[2];
 	int32_t flags;  // bit 0: producer finished, bit 1: one-token step pending
+	int32_t tail_end;        // output position just after tail[] (consumer)
+	uint8_t tail[16];        // the 16 output bytes before tail_end
 };
 
 // Consumer: copy batch `c` (records, output at o) into outb and flush it.
@@ -1111,6 +1113,13 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 {
 	const int lane = int(lane_id());
 	const int32_t nb = L.m_nb[c], blen = L.m_blen[c], o = L.m_o[c];
+	if (L.tail_end != o) {  // first batch, or output written by the one-token path
+		if (lane < 16)
+			L.tail[lane] = (o - 16 + lane >= 0) ? ob[o - 16 + lane] : 0;
+		if (lane == 0)
+			L.tail_end = o;
+		wave_mem_fence();
+	}
 	const bool tl = lane < nb;
 	const int32_t ts = tl ? L.r_tstart[c][lane] : 0;
 	const int32_t tL = tl ? L.r_L[c][lane] : 0;
@@ -1164,6 +1173,7 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 			dep &= (1ull << lane) - 1;
 		}
 	}
+	STAMP(SP_DEP);
 	bool pend = tl && tml > 0;
 	for (int guard = 0;; ++guard) {
 		const uint64_t pm = __ballot(pend);
@@ -1193,10 +1203,12 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 					lds_store_n(&L.outb[d0 + i], v, nn);
 				}
 			} else {
+				// the toff (< 16) source bytes are in this batch or in the
+				// 16-byte tail of the previous one: all LDS
 				int32_t r = 0;
 				for (int32_t k = 0; k < tml; ++k) {
 					const int32_t sp = q0 + r;
-					L.outb[d0 + k] = (sp < o) ? ob[sp] : L.outb[sp - o];
+					L.outb[d0 + k] = (sp < o) ? L.tail[sp - o + 16] : L.outb[sp - o];
 					if (++r == toff)
 						r = 0;
 				}
@@ -1221,6 +1233,15 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 		}
 		for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)
 			dst[i] = L.outb[i];
+		// keep the last 16 output bytes for the next batch's short offsets
+		uint32_t tb = 0;
+		if (lane < 16)
+			tb = (blen - 16 + lane >= 0) ? L.outb[blen - 16 + lane] : L.tail[blen + lane];
+		wave_lds_fence();
+		if (lane < 16)
+			L.tail[lane] = uint8_t(tb);
+		if (lane == 0)
+			L.tail_end = o + blen;
 	}
 	// later batches (either wave) read this output back from HBM
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1291,6 +1312,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 	if (threadIdx.x == 0) {
 		L.m_nb[0] = L.m_nb[1] = 0;
 		L.flags = pdone ? 1 : 0;
+		L.tail_end = -1;
 	}
 	__syncthreads();
 	STAMP_DECL;
@@ -1465,10 +1487,12 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 					L.m_nb[c] = 0;
 			}
 		}
+		STAMP(SP_WAIT);  // (wave's own work is stamped; this closes it)
 		__syncthreads();
 		if (threadIdx.x == 0)
 			L.flags = (pdone ? 1 : 0) | (pone ? 2 : 0);
 		__syncthreads();
+		STAMP(SP_WAIT);
 		int fl = L.flags;
 		const bool full = L.m_nb[0] > 0 || L.m_nb[1] > 0;
 		if ((fl & 2) && !full) {

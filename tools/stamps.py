@@ -19,7 +19,7 @@ import bench  # noqa: E402
 import lz4ada  # noqa: E402
 import torch  # noqa: E402
 
-PH = ["stage", "cand", "double", "select", "lit", "match", "flush", "one_token"]
+PH = ["stage", "cand", "double", "select", "lit", "match", "flush", "one_token", "wait", "dep"]
 CNT = ["batches", "windows", "tokens", "rounds"]
 
 
@@ -37,7 +37,7 @@ def main():
     st = torch.zeros(args.blocks * 32, dtype=torch.uint8, device=dev)
     f = lz4ada._lib.lz4ada_debug_stamps
     f.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 12)()
+    buf = (ctypes.c_ulonglong * 14)()
     lz4ada.launch_decode(fr.data_ptr(), fl, de.data_ptr(), args.blocks, out.data_ptr(), st.data_ptr())
     torch.cuda.synchronize()
     f(buf, 1)
@@ -48,16 +48,16 @@ def main():
     torch.cuda.synchronize()
     f(buf, 1)
     v = list(buf)
-    tot = sum(v[:8])
+    tot = sum(v[:10])
     print(f"kind={args.kind} blocks={args.blocks} kernel={e0.elapsed_time(e1):.2f} ms "
           f"(stamped build) decoded={rb / 2**20:.0f} MiB")
     for i, name in enumerate(PH):
         print(f"  {name:10s} {v[i] / args.blocks / 1e6:10.2f} Mcyc/block  {100 * v[i] / max(tot, 1):5.1f}%")
     for i, name in enumerate(CNT):
-        print(f"  {name:10s} {v[8 + i] / args.blocks:12.1f} per block")
-    nt = max(v[10], 1)
-    print(f"  cycles/token {tot / nt:.1f}   tokens/window {v[10] / max(v[9], 1):.2f}   "
-          f"tokens/batch {v[10] / max(v[8], 1):.1f}   rounds/batch {v[11] / max(v[8], 1):.2f}")
+        print(f"  {name:10s} {v[10 + i] / args.blocks:12.1f} per block")
+    nt = max(v[12], 1)
+    print(f"  cycles/token {tot / nt:.1f}   tokens/window {v[12] / max(v[11], 1):.2f}   "
+          f"tokens/batch {v[12] / max(v[10], 1):.1f}   rounds/batch {v[13] / max(v[10], 1):.2f}")
 
 
 if __name__ == "__main__":
