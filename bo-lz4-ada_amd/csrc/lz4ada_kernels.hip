@@ -1093,10 +1093,12 @@ constexpr int PC_STAGE_AHEAD = STAGE_AHEAD;
 // The ring also holds the batch the consumer is copying: the producer ends
 // its batch early (or waits a step) rather than stage over those bytes.
 
+constexpr int PC_OUTX = 16 + OUTB + 32;
+static_assert(PC_OUTX % 16 == 0, "outx is read as aligned 16-byte pairs");
+
 struct alignas(16) PcLds {
-	uint16_t J[6][WIN];
 	uint8_t inb[INB + MIRROR];
-	uint8_t outb[OUTB + 32];
+	uint8_t outx[PC_OUTX];  // [0, 16): the 16 output bytes before the batch; batch at 16
 	int32_t r_tstart[2][MAXTOK];
 	int32_t r_L[2][MAXTOK];
 	int32_t r_lit[2][MAXTOK];
@@ -1104,18 +1106,33 @@ struct alignas(16) PcLds {
 	int32_t r_ml[2][MAXTOK];
 	int32_t m_nb[2], m_blen[2], m_o[2], m_bcomp0[2];
 	int32_t flags;  // bit 0: producer finished, bit 1: one-token step pending
-	int32_t tail_end;        // output position just after tail[] (consumer)
-	uint8_t tail[16];        // the 16 output bytes before tail_end
+	int32_t tail_end;  // block output position of outx[16] (consumer)
 };
+
+// Window successor tables hold one byte per position, four positions per
+// lane (position k: lane k & 63, byte k >> 6; 0 = none).  Entry of table
+// `t` for position p, for every lane at once (p < WIN).
+__device__ __forceinline__ uint32_t win_look(uint32_t t, uint32_t p)
+{
+	const uint32_t w = uint32_t(__builtin_amdgcn_ds_bpermute(int32_t((p & 63u) << 2), int32_t(t)));
+	return (w >> (8 * ((p >> 6) & 3u))) & 0xffu;
+}
+// ... where p is itself a table entry (0 = none stays none)
+__device__ __forceinline__ uint32_t win_next(uint32_t t, uint32_t p)
+{
+	const uint32_t v = win_look(t, p);
+	return p ? v : 0u;
+}
 
 // Consumer: copy batch `c` (records, output at o) into outb and flush it.
 __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* __restrict__ ob STAMP_PARAM)
 {
 	const int lane = int(lane_id());
 	const int32_t nb = L.m_nb[c], blen = L.m_blen[c], o = L.m_o[c];
+	uint8_t* const outb = L.outx + 16;
 	if (L.tail_end != o) {  // first batch, or output written by the one-token path
 		if (lane < 16)
-			L.tail[lane] = (o - 16 + lane >= 0) ? ob[o - 16 + lane] : 0;
+			L.outx[lane] = (o - 16 + lane >= 0) ? ob[o - 16 + lane] : 0;
 		if (lane == 0)
 			L.tail_end = o;
 		wave_mem_fence();
@@ -1131,16 +1148,18 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 	u32x4 pv0 = {0, 0, 0, 0}, pv1 = {0, 0, 0, 0};
 	const bool pre0 = tl && tml > 0 && toff >= 16 && q0 + 16 <= o;
 	const bool pre1 = pre0 && tml > 16 && q0 + 32 <= o;
+#ifndef LZ4ADA_EXP_NOGLOBAL
 	if (pre0)
 		__builtin_memcpy(&pv0, (const uint8_t*)(ob + q0), 16);
 	if (pre1)
 		__builtin_memcpy(&pv1, (const uint8_t*)(ob + q0 + 16), 16);
+#endif
 	constexpr int32_t LONG = 48;
 	if (tL <= LONG) {
 		for (int32_t i = 0; i < tL; i += 16) {
 			u32x4 v;
 			__builtin_memcpy(&v, &L.inb[(tlit + i + mis) & INB_MASK], 16);
-			lds_store_n(&L.outb[ts + i], v, tL - i);
+			lds_store_n(&outb[ts + i], v, tL - i);
 		}
 	}
 	for (uint64_t lm = __ballot(tl && tL > LONG); lm; lm &= lm - 1) {
@@ -1149,7 +1168,7 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 		for (int32_t i = 16 * lane; i < Lk; i += 1024) {
 			u32x4 v;
 			__builtin_memcpy(&v, &L.inb[(litk + i + mis) & INB_MASK], 16);
-			lds_store_n(&L.outb[tsk + i], v, Lk - i);
+			lds_store_n(&outb[tsk + i], v, Lk - i);
 		}
 	}
 	wave_lds_fence();
@@ -1190,28 +1209,27 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 						v = pv0;
 					} else if (i == 16 && pre1) {
 						v = pv1;
-					} else if (sp + 16 <= o) {
-						__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
-					} else if (sp >= o) {
-						__builtin_memcpy(&v, &L.outb[sp - o], 16);
+					} else if (sp >= o - 16) {  // this batch or the tail before it
+						v = ld16u(L.outx, uint32_t(sp - o + 16), PC_OUTX);
 					} else {
-						uint8_t t[16];
-						for (int k = 0; k < 16; ++k)
-							t[k] = (sp + k < o) ? ob[sp + k] : L.outb[sp + k - o];
-						__builtin_memcpy(&v, t, 16);
+#ifdef LZ4ADA_EXP_NOGLOBAL
+						v = pv0;
+#else
+						__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
+#endif
 					}
-					lds_store_n(&L.outb[d0 + i], v, nn);
+					lds_store_n(&outb[d0 + i], v, nn);
 				}
 			} else {
 				// the toff (< 16) source bytes are in this batch or in the
-				// 16-byte tail of the previous one: all LDS
-				int32_t r = 0;
-				for (int32_t k = 0; k < tml; ++k) {
-					const int32_t sp = q0 + r;
-					L.outb[d0 + k] = (sp < o) ? L.tail[sp - o + 16] : L.outb[sp - o];
-					if (++r == toff)
-						r = 0;
-				}
+				// 16-byte tail of the previous one: a periodic fill from LDS
+				const u32x4 sv = ld16u(L.outx, uint32_t(q0 - o + 16), PC_OUTX);
+				u32x4 pv;
+				int32_t width, stp;
+				make_pattern(uint64_t(sv.x) | (uint64_t(sv.y) << 32),
+				             uint64_t(sv.z) | (uint64_t(sv.w) << 32), toff, pv, width, stp);
+				for (int32_t k = 0; k < tml; k += stp)
+					lds_store_n(&outb[d0 + k], pv, tml - k < width ? tml - k : width);
 			}
 		}
 		pend = pend && !ready;
@@ -1224,22 +1242,22 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 		const int32_t head = int32_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
 		const int32_t h = head < blen ? head : blen;
 		if (lane < h)
-			dst[lane] = L.outb[lane];
+			dst[lane] = outb[lane];
 		const int32_t nv = (blen - h) / 16;
 		for (int32_t i = lane; i < nv; i += 64) {
 			u32x4 v;
-			__builtin_memcpy(&v, &L.outb[h + 16 * i], 16);
+			__builtin_memcpy(&v, &outb[h + 16 * i], 16);
 			*reinterpret_cast<GLOBAL u32x4*>(dst + h + 16 * i) = v;
 		}
 		for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)
-			dst[i] = L.outb[i];
-		// keep the last 16 output bytes for the next batch's short offsets
+			dst[i] = outb[i];
+		// keep the last 16 output bytes in front of the next batch
 		uint32_t tb = 0;
 		if (lane < 16)
-			tb = (blen - 16 + lane >= 0) ? L.outb[blen - 16 + lane] : L.tail[blen + lane];
+			tb = L.outx[blen + lane];
 		wave_lds_fence();
 		if (lane < 16)
-			L.tail[lane] = uint8_t(tb);
+			L.outx[lane] = uint8_t(tb);
 		if (lane == 0)
 			L.tail_end = o + blen;
 	}
@@ -1381,37 +1399,49 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 							force_flush = true;
 						}
 					} else {
+						// next-token offsets of the window's WIN positions, one
+						// byte each (0: no in-window normal successor), packed
+						// four to a lane: position k in lane k & 63, byte k >> 6
+						uint32_t pk = 0;
 #pragma unroll
 						for (int q = 0; q < WIN / 64; ++q) {
 							const int k = 64 * q + lane;
 							const Cand t = parse_cand(L.inb, mis, s + k, n);
 							const int32_t rel = t.next - s;
-							L.J[0][k] = uint16_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0xffff);
+							pk |= uint32_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0) << (8 * q);
 						}
-						wave_lds_fence();
 						STAMP(SP_CAND);
+						// two doubling levels in registers (J2, J4: 2 and 4 tokens
+						// ahead), a scalar walk over J4 placing every fourth token,
+						// then each lane steps 0-3 tokens from its anchor: lane i
+						// gets the window position of the i-th token
+						uint32_t j2 = 0, j4 = 0;
 #pragma unroll
-						for (int r = 0; r < 5; ++r) {
-							uint32_t a[WIN / 64];
+						for (int q = 0; q < WIN / 64; ++q)
+							j2 |= win_next(pk, (pk >> (8 * q)) & 0xffu) << (8 * q);
 #pragma unroll
-							for (int q = 0; q < WIN / 64; ++q)
-								a[q] = L.J[r][64 * q + lane];
-#pragma unroll
-							for (int q = 0; q < WIN / 64; ++q)
-								a[q] = a[q] < WIN ? L.J[r][a[q]] : 0xffffu;
-#pragma unroll
-							for (int q = 0; q < WIN / 64; ++q)
-								L.J[r + 1][64 * q + lane] = uint16_t(a[q]);
-							wave_lds_fence();
+						for (int q = 0; q < WIN / 64; ++q)
+							j4 |= win_next(j2, (j2 >> (8 * q)) & 0xffu) << (8 * q);
+						const int32_t wl = uni(MAXTOK - nb < 64 ? MAXTOK - nb : 64);
+						uint32_t anc = 0xffffu;
+						int32_t cur = 0, walked = 0;
+						do {
+							anc = (lane == 4 * walked) ? uint32_t(cur) : anc;
+							++walked;
+							const uint32_t w = uint32_t(__builtin_amdgcn_readlane(int32_t(j4), cur & 63));
+							cur = uni(int32_t((w >> (8 * (cur >> 6))) & 0xffu));
+						} while (cur != 0 && 4 * walked < wl);
+						// quad broadcast of lane 4i's anchor (DPP quad_perm 0,0,0,0)
+						uint32_t cj = uint32_t(__builtin_amdgcn_update_dpp(0, int32_t(anc), 0x00, 0xf, 0xf, false));
+						{
+							const uint32_t x = win_look(j2, cj & 0xffu);
+							if (lane & 2)
+								cj = (cj < WIN && x) ? x : 0xffffu;
+							const uint32_t y = win_look(pk, cj & 0xffu);
+							if (lane & 1)
+								cj = (cj < WIN && y) ? y : 0xffffu;
 						}
 						STAMP(SP_DOUBLE);
-						uint32_t cj = 0;
-#pragma unroll
-						for (int r = 0; r < 6; ++r) {
-							const uint32_t g = cj < WIN ? L.J[r][cj] : 0xffffu;
-							if ((lane >> r) & 1)
-								cj = g;
-						}
 						const bool inwin = cj < WIN;
 						const Cand tk = parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
 						const int32_t kL = tk.L, klit = tk.lit, koff = tk.off, kml = tk.ml;

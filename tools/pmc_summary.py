@@ -6,7 +6,7 @@
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   profiles/<tag>_pmc.json           per-kernel counters, averaged per dispatch
-  profiles/pmc_decode.json          HBM bytes per k_decode_blocks launch, read by bench.py
+  profiles/pmc_decode.json          HBM bytes per decode launch (k_decode_pc, the default), read by bench.py
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3):
 FETCH_SIZE and WRITE_SIZE are in KiB, collected in separate --pmc passes;
@@ -23,7 +23,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_decode_blocks", "k_block_checksums", "k_output_checksums", "k_serial_block",
+KERNELS = ("k_decode_pc", "k_decode_wg", "k_decode_blocks", "k_block_checksums", "k_output_checksums", "k_serial_block",
            "k_xxh32_update", "k_compact")
 
 
@@ -86,9 +86,11 @@ def main():
     with open(os.path.join(prof, f"{args.tag}_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1)
 
-    dec = out["kernels"].get("k_decode_blocks", {})
+    dname = next((k for k in ("k_decode_pc", "k_decode_blocks") if k in out["kernels"]), None)
+    dec = out["kernels"].get(dname, {})
     if "hbm_bytes_per_launch" in dec:
         pj = {"config": {"kind": args.kind, "blocks": args.blocks, "block_max": args.block_max},
+              "kernel": dname,
               "hbm_bytes_per_launch": round(dec["hbm_bytes_per_launch"]),
               "fetch_bytes_x2": round(dec["fetch_bytes_x2"]),
               "write_bytes": round(dec["write_bytes"]),
