@@ -551,6 +551,29 @@ __device__ __forceinline__ Cand parse_cand(const uint8_t* inb, int32_t mis, int3
 	return t;
 }
 
+// parse_cand for a token at least 2 x 272 bytes before the block end, where
+// only a zero offset or a 255 extension byte (TK_ERR here; one_token
+// classifies it exactly) can make it other than TK_NORMAL.  Branch-free.
+__device__ __forceinline__ Cand parse_cand_far(const uint8_t* inb, int32_t mis, int32_t c)
+{
+	const uint32_t t2 = lds_u16(inb + ((c + mis) & INB_MASK));
+	const bool x1 = (t2 & 0xf0u) == 0xf0u, x2 = (t2 & 15u) == 15u;
+	const int32_t L = int32_t((t2 >> 4) & 15u) + int32_t(x1 ? (t2 >> 8) : 0u);
+	const int32_t lit = c + 1 + (x1 ? 1 : 0);
+	const int32_t p = lit + L;
+	const uint32_t w = lds_u32(inb + ((p + mis) & INB_MASK));
+	const uint32_t e2 = (w >> 16) & 0xffu;
+	Cand t;
+	t.L = L;
+	t.lit = lit;
+	t.off = int32_t(w & 0xffffu);
+	t.ml = int32_t(t2 & 15u) + 4 + int32_t(x2 ? e2 : 0u);
+	t.next = p + 2 + (x2 ? 1 : 0);
+	const bool ok = (t.off != 0) & !(x1 & ((t2 >> 8) == 255u)) & !(x2 & (e2 == 255u));
+	t.kind = ok ? TK_NORMAL : TK_ERR;
+	return t;
+}
+
 // Wave-uniform value: every lane holds the same; tell the compiler so it
 // keeps the serial parse in SGPRs with scalar branches.
 __device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -1090,6 +1113,19 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 constexpr int PC_BIG = BIG;            // longer sequences take the one-token path
 constexpr int PC_SPAN = SPAN;          // compressed bytes a batch may span
 constexpr int PC_STAGE_AHEAD = STAGE_AHEAD;
+#ifndef LZ4ADA_PC_SER_MIN
+#define LZ4ADA_PC_SER_MIN 64
+#endif
+// sequences averaging at least this many compressed bytes are parsed one at
+// a time (scalar); denser streams use the speculative window.  The scalar
+// parse is LDS-latency bound (~1300 cycles per sequence under load, against
+// ~420 for the window on mixed data), so only long literal runs take it.
+constexpr int PC_SER_MIN = LZ4ADA_PC_SER_MIN;
+#ifndef LZ4ADA_PC_ANCH
+#define LZ4ADA_PC_ANCH 3
+#endif
+// window walk anchors every 2^PC_ANCH sequences
+constexpr int PC_ANCH = LZ4ADA_PC_ANCH;
 // The ring also holds the batch the consumer is copying: the producer ends
 // its batch early (or waits a step) rather than stage over those bytes.
 
@@ -1108,6 +1144,64 @@ struct alignas(16) PcLds {
 	int32_t flags;  // bit 0: producer finished, bit 1: one-token step pending
 	int32_t tail_end;  // block output position of outx[16] (consumer)
 };
+
+// 8 ring bytes at block-relative x as a wave-uniform u64: three aligned
+// dword reads (the ring's 16-byte mirror covers the wrap) and a shift.
+__device__ __forceinline__ uint64_t ring_u64s(const uint8_t* inb, int32_t mis, int32_t x)
+{
+	const uint32_t a = uint32_t(x + mis) & INB_MASK;
+	const uint32_t* w = reinterpret_cast<const uint32_t*>(inb + (a & ~3u));
+	const uint32_t w0 = uint32_t(uni(int32_t(w[0])));
+	const uint32_t w1 = uint32_t(uni(int32_t(w[1])));
+	const uint32_t w2 = uint32_t(uni(int32_t(w[2])));
+	const uint32_t sh = 8u * (a & 3u);
+	const uint64_t lo = uint64_t(w0) | (uint64_t(w1) << 32);
+	return sh ? (lo >> sh) | (uint64_t(w2) << (64u - sh)) : lo;
+}
+
+// parse_serial for the common shapes with two dependent ring reads (token
+// and <= 1 extension byte, then offset and <= 1 extension byte); anything
+// else -- longer extensions, the block end, malformed data, bytes not yet
+// staged -- is left to parse_serial, so the result is the same.
+__device__ __forceinline__ bool parse_fast(const uint8_t* inb, int32_t mis, int32_t s, int32_t n,
+                                           int32_t hi, Cand& t)
+{
+	s = uni(s);
+	n = uni(n);
+	hi = uni(hi);
+	if (s + 16 > hi || s + 16 > n)
+		return parse_serial(inb, mis, s, n, hi, t);
+	const uint64_t A = ring_u64s(inb, mis, s);
+	const int32_t tk = int32_t(A & 0xffu);
+	int32_t L = tk >> 4, p = s + 1;
+	const int32_t e1 = int32_t((A >> 8) & 0xffu);
+	if (L == 15) {
+		if (e1 == 255)
+			return parse_serial(inb, mis, s, n, hi, t);
+		L += e1;
+		++p;
+	}
+	const int32_t lit = p;
+	p += L;
+	if (p + 8 > n || p + 8 > hi)
+		return parse_serial(inb, mis, s, n, hi, t);
+	const uint64_t B = (p + 3 <= s + 8) ? (A >> (8 * (p - s))) : ring_u64s(inb, mis, p);
+	const int32_t off = int32_t(B & 0xffffu), e2 = int32_t((B >> 16) & 0xffu);
+	int32_t M = tk & 15, next = p + 2;
+	if (off == 0 || (M == 15 && e2 == 255))
+		return parse_serial(inb, mis, s, n, hi, t);
+	if (M == 15) {
+		M += e2;
+		++next;
+	}
+	t.lit = lit;
+	t.L = L;
+	t.off = off;
+	t.ml = M + 4;
+	t.next = next;
+	t.kind = TK_NORMAL;
+	return true;
+}
 
 // Window successor tables hold one byte per position, four positions per
 // lane (position k: lane k & 63, byte k >> 6; 0 = none).  Entry of table
@@ -1158,7 +1252,11 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 	if (tL <= LONG) {
 		for (int32_t i = 0; i < tL; i += 16) {
 			u32x4 v;
+#ifdef LZ4ADA_EXP_LITU
+			v = ld16u(L.inb, uint32_t(tlit + i + mis) & INB_MASK, INB);
+#else
 			__builtin_memcpy(&v, &L.inb[(tlit + i + mis) & INB_MASK], 16);
+#endif
 			lds_store_n(&outb[ts + i], v, tL - i);
 		}
 	}
@@ -1167,7 +1265,11 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 		const int32_t Lk = __shfl(tL, k), litk = __shfl(tlit, k), tsk = __shfl(ts, k);
 		for (int32_t i = 16 * lane; i < Lk; i += 1024) {
 			u32x4 v;
+#ifdef LZ4ADA_EXP_LITU
+			v = ld16u(L.inb, uint32_t(litk + i + mis) & INB_MASK, INB);
+#else
 			__builtin_memcpy(&v, &L.inb[(litk + i + mis) & INB_MASK], 16);
+#endif
 			lds_store_n(&outb[tsk + i], v, Lk - i);
 		}
 	}
@@ -1246,7 +1348,11 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 		const int32_t nv = (blen - h) / 16;
 		for (int32_t i = lane; i < nv; i += 64) {
 			u32x4 v;
+#ifdef LZ4ADA_EXP_LITU
+			v = ld16u(L.outx, uint32_t(16 + h + 16 * i), PC_OUTX);
+#else
 			__builtin_memcpy(&v, &outb[h + 16 * i], 16);
+#endif
 			*reinterpret_cast<GLOBAL u32x4*>(dst + h + 16 * i) = v;
 		}
 		for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)
@@ -1327,6 +1433,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 	bool ok = true;
 	bool pdone = (n == 0);
 	bool pone = false;  // one-token step pending
+	bool smode = false;  // sequences are long: parse them one at a time
 	if (threadIdx.x == 0) {
 		L.m_nb[0] = L.m_nb[1] = 0;
 		L.flags = pdone ? 1 : 0;
@@ -1335,7 +1442,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 	__syncthreads();
 	STAMP_DECL;
 	int slot = 0;  // the producer fills `slot`, the consumer drains slot ^ 1
-	for (int32_t step = 0;; ++step) {
+	for (;;) {
 		if (wave == 0) {
 			// ------------------------------------------------ producer
 			if (!pdone && !pone) {
@@ -1370,15 +1477,27 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 					}
 					const uint32_t peek =
 					    uint32_t(uni(int32_t(lds_u16(L.inb + ((s + mis) & INB_MASK)))));
-					if ((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) {
-						Cand t = {};
-						bool okp = parse_serial(L.inb, mis, s, n, hi, t);
-						const int32_t klen = t.L + t.ml;
-						const int32_t d0 = o + blen + t.L;
-						okp = okp && nb < MAXTOK && klen <= PC_BIG && blen + klen <= OUTB &&
-						      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
-						      (t.off >= 16 || t.ml <= 64);
-						if (okp) {
+					if (((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) || smode) {
+						// serial run: one sequence at a time in scalar registers
+						// while sequences average >= PC_SER_MIN compressed bytes
+						const int32_t s_run = s;
+						int32_t took = 0;
+						for (;;) {
+							Cand t = {};
+							bool okp = parse_fast(L.inb, mis, s, n, hi, t);
+							const int32_t klen = t.L + t.ml;
+							const int32_t d0 = o + blen + t.L;
+							okp = okp && nb < MAXTOK && klen <= PC_BIG && blen + klen <= OUTB &&
+							      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
+							      (t.off >= 16 || t.ml <= 64);
+							if (!okp) {
+								if (nb == 0)
+									stop = true;
+								else
+									force_flush = true;
+								smode = false;
+								break;
+							}
 							if (lane == 0) {
 								L.r_tstart[slot][nb] = blen;
 								L.r_L[slot][nb] = t.L;
@@ -1389,61 +1508,99 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 							if (nb == 0)
 								bcomp0 = s;
 							++nb;
+							++took;
 							blen += klen;
 							STAMP_COUNT(SP_TOKENS, 1);
-							end_block = (t.kind == TK_LAST || t.next >= n);
+							if (t.kind == TK_LAST || t.next >= n) {
+								end_block = true;
+								s = t.next;
+								break;
+							}
 							s = t.next;
-						} else if (nb == 0) {
-							stop = true;
-						} else {
-							force_flush = true;
+							smode = (s - s_run) >= PC_SER_MIN * took;
+							if (!smode || nb >= MAXTOK || blen > OUTB - PC_BIG ||
+							    (s - bcomp0) >= PC_SPAN || s + PC_BIG + 64 > hi)
+								break;
 						}
 					} else {
+						const int32_t s_win = s;
 						// next-token offsets of the window's WIN positions, one
 						// byte each (0: no in-window normal successor), packed
 						// four to a lane: position k in lane k & 63, byte k >> 6
 						uint32_t pk = 0;
+						if (s + WIN + 2 * 272 < n) {
+							// far from the block end only a zero offset or a
+							// 255 extension byte can stop a chain: branch-free,
+							// all reads of a kind issued together
+							uint32_t t2[WIN / 64], w4[WIN / 64];
+							int32_t pp[WIN / 64];
 #pragma unroll
-						for (int q = 0; q < WIN / 64; ++q) {
-							const int k = 64 * q + lane;
-							const Cand t = parse_cand(L.inb, mis, s + k, n);
-							const int32_t rel = t.next - s;
-							pk |= uint32_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0) << (8 * q);
+							for (int q = 0; q < WIN / 64; ++q)
+								t2[q] = lds_u16(L.inb + ((s + 64 * q + lane + mis) & INB_MASK));
+#pragma unroll
+							for (int q = 0; q < WIN / 64; ++q) {
+								const uint32_t x1 = ((t2[q] & 0xf0u) == 0xf0u) ? 1u : 0u;
+								pp[q] = 64 * q + lane + 1 + int32_t(x1) + int32_t((t2[q] >> 4) & 15u) +
+								        int32_t(x1 ? (t2[q] >> 8) : 0u);
+							}
+#pragma unroll
+							for (int q = 0; q < WIN / 64; ++q)
+								w4[q] = lds_u32(L.inb + ((s + pp[q] + mis) & INB_MASK));
+#pragma unroll
+							for (int q = 0; q < WIN / 64; ++q) {
+								const bool x1 = (t2[q] & 0xf0u) == 0xf0u, x2 = (t2[q] & 15u) == 15u;
+								const uint32_t e2 = (w4[q] >> 16) & 0xffu;
+								const int32_t rel = pp[q] + 2 + (x2 ? 1 : 0);
+								const bool ok = ((w4[q] & 0xffffu) != 0) & !(x1 & ((t2[q] >> 8) == 255u)) &
+								                !(x2 & (e2 == 255u)) & (rel < WIN);
+								pk |= uint32_t(ok ? rel : 0) << (8 * q);
+							}
+						} else {
+#pragma unroll
+							for (int q = 0; q < WIN / 64; ++q) {
+								const int k = 64 * q + lane;
+								const Cand t = parse_cand(L.inb, mis, s + k, n);
+								const int32_t rel = t.next - s;
+								pk |= uint32_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0) << (8 * q);
+							}
 						}
 						STAMP(SP_CAND);
-						// two doubling levels in registers (J2, J4: 2 and 4 tokens
-						// ahead), a scalar walk over J4 placing every fourth token,
-						// then each lane steps 0-3 tokens from its anchor: lane i
-						// gets the window position of the i-th token
-						uint32_t j2 = 0, j4 = 0;
+						// PC_ANCH doubling levels in registers (tables 2, 4, ..
+						// 2^PC_ANCH sequences ahead), a scalar walk over the last
+						// placing every 2^PC_ANCH-th sequence in its lane group,
+						// then each lane steps from that anchor by the binary
+						// digits of its index: lane i gets sequence i's position
+						uint32_t jt[PC_ANCH + 1];
+						jt[0] = pk;
 #pragma unroll
-						for (int q = 0; q < WIN / 64; ++q)
-							j2 |= win_next(pk, (pk >> (8 * q)) & 0xffu) << (8 * q);
+						for (int r = 1; r <= PC_ANCH; ++r) {
+							uint32_t j = 0;
 #pragma unroll
-						for (int q = 0; q < WIN / 64; ++q)
-							j4 |= win_next(j2, (j2 >> (8 * q)) & 0xffu) << (8 * q);
+							for (int q = 0; q < WIN / 64; ++q)
+								j |= win_next(jt[r - 1], (jt[r - 1] >> (8 * q)) & 0xffu) << (8 * q);
+							jt[r] = j;
+						}
 						const int32_t wl = uni(MAXTOK - nb < 64 ? MAXTOK - nb : 64);
-						uint32_t anc = 0xffffu;
+						uint32_t cj = 0xffffu;
 						int32_t cur = 0, walked = 0;
 						do {
-							anc = (lane == 4 * walked) ? uint32_t(cur) : anc;
+							cj = ((lane >> PC_ANCH) == walked) ? uint32_t(cur) : cj;
 							++walked;
-							const uint32_t w = uint32_t(__builtin_amdgcn_readlane(int32_t(j4), cur & 63));
+							const uint32_t w =
+							    uint32_t(__builtin_amdgcn_readlane(int32_t(jt[PC_ANCH]), cur & 63));
 							cur = uni(int32_t((w >> (8 * (cur >> 6))) & 0xffu));
-						} while (cur != 0 && 4 * walked < wl);
-						// quad broadcast of lane 4i's anchor (DPP quad_perm 0,0,0,0)
-						uint32_t cj = uint32_t(__builtin_amdgcn_update_dpp(0, int32_t(anc), 0x00, 0xf, 0xf, false));
-						{
-							const uint32_t x = win_look(j2, cj & 0xffu);
-							if (lane & 2)
+						} while (cur != 0 && (walked << PC_ANCH) < wl);
+#pragma unroll
+						for (int r = PC_ANCH - 1; r >= 0; --r) {
+							const uint32_t x = win_look(jt[r], cj & 0xffu);
+							if ((lane >> r) & 1)
 								cj = (cj < WIN && x) ? x : 0xffffu;
-							const uint32_t y = win_look(pk, cj & 0xffu);
-							if (lane & 1)
-								cj = (cj < WIN && y) ? y : 0xffffu;
 						}
 						STAMP(SP_DOUBLE);
 						const bool inwin = cj < WIN;
-						const Cand tk = parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
+						const Cand tk = (s + WIN + 2 * 272 < n)
+						                    ? parse_cand_far(L.inb, mis, s + (inwin ? int32_t(cj) : 0))
+						                    : parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
 						const int32_t kL = tk.L, klit = tk.lit, koff = tk.off, kml = tk.ml;
 						const int32_t knext = tk.next, kkind = tk.kind;
 						const bool good = inwin && (kkind == TK_NORMAL || kkind == TK_LAST);
@@ -1467,6 +1624,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 							L.r_ml[slot][nb + lane] = kml;
 						}
 						STAMP_COUNT(SP_TOKENS, cnt);
+						smode = cnt > 0 && cnext - s_win >= PC_SER_MIN * cnt;
 						const bool was_empty = (nb == 0);
 						if (was_empty && cnt > 0)
 							bcomp0 = s;
@@ -1489,7 +1647,8 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 					wave_lds_fence();
 					STAMP(SP_SELECT);
 					const bool flush = end_block || stop || force_flush ||
-					                   nb > MAXTOK - WTOK / 2 || blen > OUTB - PC_BIG ||
+					                   nb > (smode ? MAXTOK - 1 : MAXTOK - WTOK / 2) ||
+					                   blen > OUTB - PC_BIG ||
 					                   (s - bcomp0) >= PC_SPAN;
 					if (flush) {
 						if (lane == 0) {
