@@ -655,6 +655,66 @@ static int guarded(std::string* err, F&& f)
 	}
 }
 
+// XXHash32.Update / Final (lz4ada.adb:942-1017) on host bytes, for the
+// content checksum pipeline only; the state layout is the one the GPU
+// kernel k_xxh32_update advances, so the two can continue each other.
+static inline uint32_t rotl32h(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static inline uint32_t xxh_round(uint32_t acc, uint32_t w) { return rotl32h(acc + w * P2, 13) * P1; }
+
+static void host_xxh32_update(lz4ada_xxh32_state& h, const uint8_t* p, size_t n)
+{
+	h.total_length += n;
+	size_t bs = size_t(h.buffer_size);
+	if (bs + n < 16) {
+		if (n)
+			memcpy(h.buffer + bs, p, n);
+		h.buffer_size = int32_t(bs + n);
+		return;
+	}
+	if (bs) {  // complete the buffered stripe (Update1, :965-991)
+		const size_t k = 16 - bs;
+		memcpy(h.buffer + bs, p, k);
+		p += k;
+		n -= k;
+		for (int i = 0; i < 4; ++i)
+			h.state[i] = xxh_round(h.state[i], load32(h.buffer + 4 * i));
+	}
+	uint32_t v0 = h.state[0], v1 = h.state[1], v2 = h.state[2], v3 = h.state[3];
+	for (; n >= 16; p += 16, n -= 16) {  // stripes (Process, :951-958)
+		v0 = xxh_round(v0, load32(p));
+		v1 = xxh_round(v1, load32(p + 4));
+		v2 = xxh_round(v2, load32(p + 8));
+		v3 = xxh_round(v3, load32(p + 12));
+	}
+	h.state[0] = v0;
+	h.state[1] = v1;
+	h.state[2] = v2;
+	h.state[3] = v3;
+	if (n)
+		memcpy(h.buffer, p, n);
+	h.buffer_size = int32_t(n);
+}
+
+static uint32_t host_xxh32_final(const lz4ada_xxh32_state& h)  // :993-1017
+{
+	uint32_t acc = h.total_length >= 16 ? rotl32h(h.state[0], 1) + rotl32h(h.state[1], 7) +
+	                                          rotl32h(h.state[2], 12) + rotl32h(h.state[3], 18)
+	                                    : h.state[2] + P5;
+	acc += uint32_t(h.total_length);
+	const uint8_t* p = h.buffer;
+	size_t n = size_t(h.buffer_size);
+	for (; n >= 4; p += 4, n -= 4)
+		acc = rotl32h(acc + load32(p) * P3, 17) * P4;
+	for (; n; ++p, --n)
+		acc = rotl32h(acc + uint32_t(*p) * P5, 11) * P1;
+	acc ^= acc >> 15;
+	acc *= P2;
+	acc ^= acc >> 13;
+	acc *= P3;
+	acc ^= acc >> 16;
+	return acc;
+}
+
 static lz4ada_decompressor* new_ctx(int64_t in_last)
 {
 	auto* c = new lz4ada_decompressor();
@@ -842,6 +902,63 @@ uint32_t lz4ada_xxh32_final(const lz4ada_xxh32_state* h)
 			return 0;
 	}
 	return t.hash;
+}
+
+// Content checksum pipeline: the frame-wide XXH32 is
+// one serial chain that one GPU wave runs at ~1.3 GB/s, so
+// for output that is headed to the host anyway the chain runs on the host
+// core, chunk by chunk, while the next chunk is still in flight over PCIe.
+// The bytes hashed are the ones the GPU decoded; nothing is decoded here.
+static void content_xxh32_d2h(lz4ada_xxh32_state& h, const uint8_t* d_data, int64_t len,
+                              uint8_t* host_out, hipStream_t stream)
+{
+	device_check_or_raise();
+	constexpr size_t CH = size_t(32) << 20;
+	struct Pinned {
+		uint8_t* p[2] = { nullptr, nullptr };
+		hipEvent_t ev[2] = { nullptr, nullptr };
+		~Pinned()
+		{
+			for (int i = 0; i < 2; ++i) {
+				if (p[i])
+					(void)hipHostFree(p[i]);
+				if (ev[i])
+					(void)hipEventDestroy(ev[i]);
+			}
+		}
+	} pin;
+	const size_t n = size_t(std::max<int64_t>(len, 0));
+	const size_t chunks = (n + CH - 1) / CH;
+	for (int i = 0; i < 2 && size_t(i) < chunks; ++i) {
+		HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&pin.p[i]), CH, hipHostMallocDefault));
+		HIP_OK(hipEventCreateWithFlags(&pin.ev[i], hipEventDisableTiming));
+	}
+	auto issue = [&](size_t k) {
+		const size_t off = k * CH, c = std::min(CH, n - off);
+		HIP_OK(hipMemcpyAsync(pin.p[k & 1], d_data + off, c, hipMemcpyDeviceToHost, stream));
+		HIP_OK(hipEventRecord(pin.ev[k & 1], stream));
+	};
+	if (chunks)
+		issue(0);
+	for (size_t k = 0; k < chunks; ++k) {
+		if (k + 1 < chunks)
+			issue(k + 1);  // in flight while chunk k is hashed
+		HIP_OK(hipEventSynchronize(pin.ev[k & 1]));
+		const size_t off = k * CH, c = std::min(CH, n - off);
+		host_xxh32_update(h, pin.p[k & 1], c);
+		if (host_out)
+			memcpy(host_out + off, pin.p[k & 1], c);
+	}
+	h.hash = host_xxh32_final(h);
+}
+
+int lz4ada_content_xxh32_d2h(lz4ada_xxh32_state* h, const void* d_data, int64_t len,
+                             uint8_t* host_out, void* stream)
+{
+	return guarded(nullptr, [&] {
+		content_xxh32_d2h(*h, static_cast<const uint8_t*>(d_data), len, host_out,
+		                  static_cast<hipStream_t>(stream));
+	});
 }
 
 int lz4ada_xxh32_hash(const uint8_t* data, int64_t len, uint32_t* out)
@@ -1047,18 +1164,15 @@ static bool fast_frame(const uint8_t* f, int64_t len, const lz4ada_frame_info& i
 		d_res = d_compact.p;
 	}
 	if (info.content_checksum) {
+		// D2H overlapped with the host XXH32 chain (content_xxh32_d2h)
 		lz4ada_xxh32_state h;
 		lz4ada_xxh32_reset(&h, 0);
-		DevBuf<lz4ada_xxh32_state> d_h;
-		d_h.reserve(1);
-		HIP_OK(hipMemcpy(d_h.p, &h, sizeof h, hipMemcpyHostToDevice));
-		HIP_OK(launch_xxh32_update(d_h.p, d_res, total, stream));
-		HIP_OK(hipMemcpy(&h, d_h.p, sizeof h, hipMemcpyDeviceToHost));
+		content_xxh32_d2h(h, d_res, int64_t(total), out, stream);
 		if (h.hash != info.content_checksum_declared)
 			return false;
-	}
-	if (total)
+	} else if (total) {
 		HIP_OK(hipMemcpy(out, d_res, size_t(total), hipMemcpyDeviceToHost));
+	}
 	out_len = int64_t(total);
 	return true;
 }

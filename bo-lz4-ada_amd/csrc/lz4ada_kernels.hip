@@ -1132,18 +1132,31 @@ constexpr int PC_ANCH = LZ4ADA_PC_ANCH;
 constexpr int PC_OUTX = 16 + OUTB + 32;
 static_assert(PC_OUTX % 16 == 0, "outx is read as aligned 16-byte pairs");
 
+#ifndef LZ4ADA_PC_SLOTS
+#define LZ4ADA_PC_SLOTS 4
+#endif
+// record slots between producer and consumer (a power of two)
+constexpr int PC_SLOTS = LZ4ADA_PC_SLOTS;
+static_assert((PC_SLOTS & (PC_SLOTS - 1)) == 0 && PC_SLOTS >= 2, "PC_SLOTS: power of two >= 2");
+
 struct alignas(16) PcLds {
 	uint8_t inb[INB + MIRROR];
 	uint8_t outx[PC_OUTX];  // [0, 16): the 16 output bytes before the batch; batch at 16
-	int32_t r_tstart[2][MAXTOK];
-	int32_t r_L[2][MAXTOK];
-	int32_t r_lit[2][MAXTOK];
-	int32_t r_off[2][MAXTOK];
-	int32_t r_ml[2][MAXTOK];
-	int32_t m_nb[2], m_blen[2], m_o[2], m_bcomp0[2];
-	int32_t flags;  // bit 0: producer finished, bit 1: one-token step pending
-	int32_t tail_end;  // block output position of outx[16] (consumer)
+	int32_t r_tstart[PC_SLOTS][MAXTOK];
+	int32_t r_L[PC_SLOTS][MAXTOK];
+	int32_t r_lit[PC_SLOTS][MAXTOK];
+	int32_t r_off[PC_SLOTS][MAXTOK];
+	int32_t r_ml[PC_SLOTS][MAXTOK];
+	int32_t m_nb[PC_SLOTS], m_blen[PC_SLOTS], m_o[PC_SLOTS], m_bcomp0[PC_SLOTS];
+	int32_t full[PC_SLOTS];  // 1: the slot's records wait for (or are being copied by) the consumer
+	int32_t pdone;           // producer finished: no slot will be filled again
+	int32_t tail_end;        // block output position of outx[16] (consumer)
 };
+
+__device__ __forceinline__ int32_t lds_poll(const int32_t* p)
+{
+	return *reinterpret_cast<const volatile int32_t*>(p);
+}
 
 // 8 ring bytes at block-relative x as a wave-uniform u64: three aligned
 // dword reads (the ring's 16-byte mirror covers the wrap) and a shift.
@@ -1219,6 +1232,20 @@ __device__ __forceinline__ uint32_t win_next(uint32_t t, uint32_t p)
 }
 
 // Consumer: copy batch `c` (records, output at o) into outb and flush it.
+// Timing experiments only (wrong output): LZ4ADA_EXP_ALIGNST stores every
+// copy chunk as one aligned 16-byte write, LZ4ADA_EXP_ALIGNLD reads literal
+// chunks from aligned addresses -- the cost of unaligned LDS access.
+#ifdef LZ4ADA_EXP_ALIGNST
+#define PC_STORE_N(p, v, n) (*reinterpret_cast<u32x4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15)) = (v))
+#else
+#define PC_STORE_N(p, v, n) lds_store_n((p), (v), (n))
+#endif
+#ifdef LZ4ADA_EXP_ALIGNLD
+#define PC_LOAD16(dst, p) (*(dst) = *reinterpret_cast<const u32x4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15)))
+#else
+#define PC_LOAD16(dst, p) __builtin_memcpy((dst), (p), 16)
+#endif
+
 __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* __restrict__ ob STAMP_PARAM)
 {
 	const int lane = int(lane_id());
@@ -1255,9 +1282,9 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 #ifdef LZ4ADA_EXP_LITU
 			v = ld16u(L.inb, uint32_t(tlit + i + mis) & INB_MASK, INB);
 #else
-			__builtin_memcpy(&v, &L.inb[(tlit + i + mis) & INB_MASK], 16);
+			PC_LOAD16(&v, &L.inb[(tlit + i + mis) & INB_MASK]);
 #endif
-			lds_store_n(&outb[ts + i], v, tL - i);
+			PC_STORE_N(&outb[ts + i], v, tL - i);
 		}
 	}
 	for (uint64_t lm = __ballot(tl && tL > LONG); lm; lm &= lm - 1) {
@@ -1268,9 +1295,9 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 #ifdef LZ4ADA_EXP_LITU
 			v = ld16u(L.inb, uint32_t(litk + i + mis) & INB_MASK, INB);
 #else
-			__builtin_memcpy(&v, &L.inb[(litk + i + mis) & INB_MASK], 16);
+			PC_LOAD16(&v, &L.inb[(litk + i + mis) & INB_MASK]);
 #endif
-			lds_store_n(&outb[tsk + i], v, Lk - i);
+			PC_STORE_N(&outb[tsk + i], v, Lk - i);
 		}
 	}
 	wave_lds_fence();
@@ -1320,7 +1347,7 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 						__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
 #endif
 					}
-					lds_store_n(&outb[d0 + i], v, nn);
+					PC_STORE_N(&outb[d0 + i], v, nn);
 				}
 			} else {
 				// the toff (< 16) source bytes are in this batch or in the
@@ -1331,7 +1358,7 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 				make_pattern(uint64_t(sv.x) | (uint64_t(sv.y) << 32),
 				             uint64_t(sv.z) | (uint64_t(sv.w) << 32), toff, pv, width, stp);
 				for (int32_t k = 0; k < tml; k += stp)
-					lds_store_n(&outb[d0 + k], pv, tml - k < width ? tml - k : width);
+					PC_STORE_N(&outb[d0 + k], pv, tml - k < width ? tml - k : width);
 			}
 		}
 		pend = pend && !ready;
@@ -1432,261 +1459,259 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 	}
 	bool ok = true;
 	bool pdone = (n == 0);
-	bool pone = false;  // one-token step pending
 	bool smode = false;  // sequences are long: parse them one at a time
+	if (threadIdx.x < PC_SLOTS)
+		L.full[threadIdx.x] = 0;
 	if (threadIdx.x == 0) {
-		L.m_nb[0] = L.m_nb[1] = 0;
-		L.flags = pdone ? 1 : 0;
+		L.pdone = pdone ? 1 : 0;
 		L.tail_end = -1;
 	}
 	__syncthreads();
 	STAMP_DECL;
-	int slot = 0;  // the producer fills `slot`, the consumer drains slot ^ 1
-	for (;;) {
-		if (wave == 0) {
-			// ------------------------------------------------ producer
-			if (!pdone && !pone) {
-				const int c = slot ^ 1;
-				const int32_t keep = L.m_nb[c] > 0 ? L.m_bcomp0[c] : INT32_MAX;
-				int32_t nb = 0, blen = 0, bcomp0 = s;
-				for (int32_t iter = 0;; ++iter) {
-					if (iter > 4 * n + 64) {
-						st.code = DS_INTERNAL;
-						ok = false;
-						pdone = true;
+	// The waves share only the slot queue: the producer fills slot pseq
+	// (mod PC_SLOTS) once the consumer has released it and raises its
+	// `full` flag; the consumer copies the slots in order and lowers the
+	// flag after its flush has reached memory.  No workgroup barriers.
+	if (wave == 0) {
+		// ---------------------------------------------------- producer
+		int32_t pseq = 0;
+		while (!pdone) {
+			const int ps = pseq & (PC_SLOTS - 1);
+			while (lds_poll(&L.full[ps]))
+				__builtin_amdgcn_s_sleep(1);
+			STAMP(SP_WAIT);
+			int32_t nb = 0, blen = 0, bcomp0 = s;
+			bool stop = false, end_block = false;
+			for (int32_t iter = 0;; ++iter) {
+				if (iter > 4 * n + 64) {
+					st.code = DS_INTERNAL;
+					ok = false;
+					pdone = true;
+					break;
+				}
+				// oldest compressed byte a queued batch may still read
+				int32_t keep = INT32_MAX;
+#pragma unroll
+				for (int k = 1; k < PC_SLOTS; ++k) {
+					const int q = (pseq - k) & (PC_SLOTS - 1);
+					if (lds_poll(&L.full[q]))
+						keep = L.m_bcomp0[q] < keep ? L.m_bcomp0[q] : keep;
+				}
+				keep = uni(keep);
+				if (keep != INT32_MAX && s + PC_STAGE_AHEAD + 1024 + MIRROR - keep > INB) {
+					// staging further would overwrite a queued batch's input
+					if (nb > 0)
 						break;
-					}
-					bool stop = false, end_block = false, force_flush = false;
-					if (keep != INT32_MAX && s + PC_STAGE_AHEAD + 1024 + MIRROR - keep > INB) {
-						// staging further would overwrite the consumer's batch
-						if (lane == 0) {
-							L.m_nb[slot] = nb;
-							L.m_blen[slot] = blen;
-							L.m_o[slot] = o;
-							L.m_bcomp0[slot] = bcomp0;
-						}
-						o += blen;
-						break;
-					}
-					{
-						int32_t lo = nb ? bcomp0 : s;
-						lo = keep < lo ? keep : lo;
-						stage_to(L, in, lim_addr, mis, hi, pf0, pf1, lo, s + PC_STAGE_AHEAD);
-						STAMP(SP_STAGE);
-						STAMP_COUNT(SP_WINDOWS, 1);
-					}
-					const uint32_t peek =
-					    uint32_t(uni(int32_t(lds_u16(L.inb + ((s + mis) & INB_MASK)))));
-					if (((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) || smode) {
-						// serial run: one sequence at a time in scalar registers
-						// while sequences average >= PC_SER_MIN compressed bytes
-						const int32_t s_run = s;
-						int32_t took = 0;
-						for (;;) {
-							Cand t = {};
-							bool okp = parse_fast(L.inb, mis, s, n, hi, t);
-							const int32_t klen = t.L + t.ml;
-							const int32_t d0 = o + blen + t.L;
-							okp = okp && nb < MAXTOK && klen <= PC_BIG && blen + klen <= OUTB &&
-							      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
-							      (t.off >= 16 || t.ml <= 64);
-							if (!okp) {
-								if (nb == 0)
-									stop = true;
-								else
-									force_flush = true;
-								smode = false;
-								break;
-							}
-							if (lane == 0) {
-								L.r_tstart[slot][nb] = blen;
-								L.r_L[slot][nb] = t.L;
-								L.r_lit[slot][nb] = t.lit;
-								L.r_off[slot][nb] = t.off;
-								L.r_ml[slot][nb] = t.ml;
-							}
+					__builtin_amdgcn_s_sleep(2);
+					--iter;
+					continue;
+				}
+				bool force_flush = false;
+				{
+					int32_t lo = nb ? bcomp0 : s;
+					lo = keep < lo ? keep : lo;
+					stage_to(L, in, lim_addr, mis, hi, pf0, pf1, lo, s + PC_STAGE_AHEAD);
+					STAMP(SP_STAGE);
+					STAMP_COUNT(SP_WINDOWS, 1);
+				}
+				const uint32_t peek =
+				    uint32_t(uni(int32_t(lds_u16(L.inb + ((s + mis) & INB_MASK)))));
+				if (((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) || smode) {
+					// serial run: one sequence at a time in scalar registers
+					// while sequences average >= PC_SER_MIN compressed bytes
+					const int32_t s_run = s;
+					int32_t took = 0;
+					for (;;) {
+						Cand t = {};
+						bool okp = parse_fast(L.inb, mis, s, n, hi, t);
+						const int32_t klen = t.L + t.ml;
+						const int32_t d0 = o + blen + t.L;
+						okp = okp && nb < MAXTOK && klen <= PC_BIG && blen + klen <= OUTB &&
+						      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
+						      (t.off >= 16 || t.ml <= 64);
+						if (!okp) {
 							if (nb == 0)
-								bcomp0 = s;
-							++nb;
-							++took;
-							blen += klen;
-							STAMP_COUNT(SP_TOKENS, 1);
-							if (t.kind == TK_LAST || t.next >= n) {
-								end_block = true;
-								s = t.next;
-								break;
-							}
+								stop = true;
+							else
+								force_flush = true;
+							smode = false;
+							break;
+						}
+						if (lane == 0) {
+							L.r_tstart[ps][nb] = blen;
+							L.r_L[ps][nb] = t.L;
+							L.r_lit[ps][nb] = t.lit;
+							L.r_off[ps][nb] = t.off;
+							L.r_ml[ps][nb] = t.ml;
+						}
+						if (nb == 0)
+							bcomp0 = s;
+						++nb;
+						++took;
+						blen += klen;
+						STAMP_COUNT(SP_TOKENS, 1);
+						if (t.kind == TK_LAST || t.next >= n) {
+							end_block = true;
 							s = t.next;
-							smode = (s - s_run) >= PC_SER_MIN * took;
-							if (!smode || nb >= MAXTOK || blen > OUTB - PC_BIG ||
-							    (s - bcomp0) >= PC_SPAN || s + PC_BIG + 64 > hi)
-								break;
+							break;
+						}
+						s = t.next;
+						smode = (s - s_run) >= PC_SER_MIN * took;
+						if (!smode || nb >= MAXTOK || blen > OUTB - PC_BIG ||
+						    (s - bcomp0) >= PC_SPAN || s + PC_BIG + 64 > hi)
+							break;
+					}
+				} else {
+					const int32_t s_win = s;
+					// next-token offsets of the window's WIN positions, one
+					// byte each (0: no in-window normal successor), packed
+					// four to a lane: position k in lane k & 63, byte k >> 6
+					uint32_t pk = 0;
+					if (s + WIN + 2 * 272 < n) {
+						// far from the block end only a zero offset or a
+						// 255 extension byte can stop a chain: branch-free,
+						// all reads of a kind issued together
+						uint32_t t2[WIN / 64], w4[WIN / 64];
+						int32_t pp[WIN / 64];
+#pragma unroll
+						for (int q = 0; q < WIN / 64; ++q)
+							t2[q] = lds_u16(L.inb + ((s + 64 * q + lane + mis) & INB_MASK));
+#pragma unroll
+						for (int q = 0; q < WIN / 64; ++q) {
+							const uint32_t x1 = ((t2[q] & 0xf0u) == 0xf0u) ? 1u : 0u;
+							pp[q] = 64 * q + lane + 1 + int32_t(x1) + int32_t((t2[q] >> 4) & 15u) +
+							        int32_t(x1 ? (t2[q] >> 8) : 0u);
+						}
+#pragma unroll
+						for (int q = 0; q < WIN / 64; ++q)
+							w4[q] = lds_u32(L.inb + ((s + pp[q] + mis) & INB_MASK));
+#pragma unroll
+						for (int q = 0; q < WIN / 64; ++q) {
+							const bool x1 = (t2[q] & 0xf0u) == 0xf0u, x2 = (t2[q] & 15u) == 15u;
+							const uint32_t e2 = (w4[q] >> 16) & 0xffu;
+							const int32_t rel = pp[q] + 2 + (x2 ? 1 : 0);
+							const bool ok = ((w4[q] & 0xffffu) != 0) & !(x1 & ((t2[q] >> 8) == 255u)) &
+							                !(x2 & (e2 == 255u)) & (rel < WIN);
+							pk |= uint32_t(ok ? rel : 0) << (8 * q);
 						}
 					} else {
-						const int32_t s_win = s;
-						// next-token offsets of the window's WIN positions, one
-						// byte each (0: no in-window normal successor), packed
-						// four to a lane: position k in lane k & 63, byte k >> 6
-						uint32_t pk = 0;
-						if (s + WIN + 2 * 272 < n) {
-							// far from the block end only a zero offset or a
-							// 255 extension byte can stop a chain: branch-free,
-							// all reads of a kind issued together
-							uint32_t t2[WIN / 64], w4[WIN / 64];
-							int32_t pp[WIN / 64];
 #pragma unroll
-							for (int q = 0; q < WIN / 64; ++q)
-								t2[q] = lds_u16(L.inb + ((s + 64 * q + lane + mis) & INB_MASK));
-#pragma unroll
-							for (int q = 0; q < WIN / 64; ++q) {
-								const uint32_t x1 = ((t2[q] & 0xf0u) == 0xf0u) ? 1u : 0u;
-								pp[q] = 64 * q + lane + 1 + int32_t(x1) + int32_t((t2[q] >> 4) & 15u) +
-								        int32_t(x1 ? (t2[q] >> 8) : 0u);
-							}
-#pragma unroll
-							for (int q = 0; q < WIN / 64; ++q)
-								w4[q] = lds_u32(L.inb + ((s + pp[q] + mis) & INB_MASK));
-#pragma unroll
-							for (int q = 0; q < WIN / 64; ++q) {
-								const bool x1 = (t2[q] & 0xf0u) == 0xf0u, x2 = (t2[q] & 15u) == 15u;
-								const uint32_t e2 = (w4[q] >> 16) & 0xffu;
-								const int32_t rel = pp[q] + 2 + (x2 ? 1 : 0);
-								const bool ok = ((w4[q] & 0xffffu) != 0) & !(x1 & ((t2[q] >> 8) == 255u)) &
-								                !(x2 & (e2 == 255u)) & (rel < WIN);
-								pk |= uint32_t(ok ? rel : 0) << (8 * q);
-							}
-						} else {
-#pragma unroll
-							for (int q = 0; q < WIN / 64; ++q) {
-								const int k = 64 * q + lane;
-								const Cand t = parse_cand(L.inb, mis, s + k, n);
-								const int32_t rel = t.next - s;
-								pk |= uint32_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0) << (8 * q);
-							}
-						}
-						STAMP(SP_CAND);
-						// PC_ANCH doubling levels in registers (tables 2, 4, ..
-						// 2^PC_ANCH sequences ahead), a scalar walk over the last
-						// placing every 2^PC_ANCH-th sequence in its lane group,
-						// then each lane steps from that anchor by the binary
-						// digits of its index: lane i gets sequence i's position
-						uint32_t jt[PC_ANCH + 1];
-						jt[0] = pk;
-#pragma unroll
-						for (int r = 1; r <= PC_ANCH; ++r) {
-							uint32_t j = 0;
-#pragma unroll
-							for (int q = 0; q < WIN / 64; ++q)
-								j |= win_next(jt[r - 1], (jt[r - 1] >> (8 * q)) & 0xffu) << (8 * q);
-							jt[r] = j;
-						}
-						const int32_t wl = uni(MAXTOK - nb < 64 ? MAXTOK - nb : 64);
-						uint32_t cj = 0xffffu;
-						int32_t cur = 0, walked = 0;
-						do {
-							cj = ((lane >> PC_ANCH) == walked) ? uint32_t(cur) : cj;
-							++walked;
-							const uint32_t w =
-							    uint32_t(__builtin_amdgcn_readlane(int32_t(jt[PC_ANCH]), cur & 63));
-							cur = uni(int32_t((w >> (8 * (cur >> 6))) & 0xffu));
-						} while (cur != 0 && (walked << PC_ANCH) < wl);
-#pragma unroll
-						for (int r = PC_ANCH - 1; r >= 0; --r) {
-							const uint32_t x = win_look(jt[r], cj & 0xffu);
-							if ((lane >> r) & 1)
-								cj = (cj < WIN && x) ? x : 0xffffu;
-						}
-						STAMP(SP_DOUBLE);
-						const bool inwin = cj < WIN;
-						const Cand tk = (s + WIN + 2 * 272 < n)
-						                    ? parse_cand_far(L.inb, mis, s + (inwin ? int32_t(cj) : 0))
-						                    : parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
-						const int32_t kL = tk.L, klit = tk.lit, koff = tk.off, kml = tk.ml;
-						const int32_t knext = tk.next, kkind = tk.kind;
-						const bool good = inwin && (kkind == TK_NORMAL || kkind == TK_LAST);
-						const int32_t klen = kL + kml;
-						const int32_t incl = wave_incl_scan(good ? klen : 0);
-						const int32_t tstart = blen + incl - klen;
-						const int32_t d0 = o + tstart + kL;
-						const bool fits = good && lane < MAXTOK - nb && klen <= PC_BIG &&
-						                  blen + incl <= OUTB && o + blen + incl <= cap &&
-						                  (kkind != TK_NORMAL || d0 - koff >= 0) &&
-						                  (koff >= 16 || kml <= 64);
-						const uint64_t badm = __ballot(!fits);
-						const int cnt = badm ? (__ffsll((long long)badm) - 1) : 64;
-						const int32_t cnext = cnt > 0 ? __shfl(knext, cnt - 1) : s;
-						const int32_t ckind_last = cnt > 0 ? __shfl(kkind, cnt - 1) : TK_NORMAL;
-						if (lane < cnt) {
-							L.r_tstart[slot][nb + lane] = tstart;
-							L.r_L[slot][nb + lane] = kL;
-							L.r_lit[slot][nb + lane] = klit;
-							L.r_off[slot][nb + lane] = koff;
-							L.r_ml[slot][nb + lane] = kml;
-						}
-						STAMP_COUNT(SP_TOKENS, cnt);
-						smode = cnt > 0 && cnext - s_win >= PC_SER_MIN * cnt;
-						const bool was_empty = (nb == 0);
-						if (was_empty && cnt > 0)
-							bcomp0 = s;
-						nb += cnt;
-						blen += cnt > 0 ? __shfl(incl, cnt - 1) : 0;
-						if (cnt > 0 && ckind_last == TK_LAST) {
-							end_block = true;
-							s = n;
-						} else if (cnt > 0 && cnext >= n) {
-							end_block = true;  // block ends right after a match (lz4ada.adb:780)
-							s = cnext;
-						} else if (cnt > 0) {
-							s = cnext;
-						} else if (was_empty) {
-							stop = true;
-						} else {
-							force_flush = true;
+						for (int q = 0; q < WIN / 64; ++q) {
+							const int k = 64 * q + lane;
+							const Cand t = parse_cand(L.inb, mis, s + k, n);
+							const int32_t rel = t.next - s;
+							pk |= uint32_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0) << (8 * q);
 						}
 					}
-					wave_lds_fence();
-					STAMP(SP_SELECT);
-					const bool flush = end_block || stop || force_flush ||
-					                   nb > (smode ? MAXTOK - 1 : MAXTOK - WTOK / 2) ||
-					                   blen > OUTB - PC_BIG ||
-					                   (s - bcomp0) >= PC_SPAN;
-					if (flush) {
-						if (lane == 0) {
-							L.m_nb[slot] = nb;
-							L.m_blen[slot] = blen;
-							L.m_o[slot] = o;
-							L.m_bcomp0[slot] = bcomp0;
-						}
-						o += blen;
-						if (end_block)
-							pdone = true;
-						if (stop)
-							pone = true;
-						break;
+					STAMP(SP_CAND);
+					// PC_ANCH doubling levels in registers (tables 2, 4, ..
+					// 2^PC_ANCH sequences ahead), a scalar walk over the last
+					// placing every 2^PC_ANCH-th sequence in its lane group,
+					// then each lane steps from that anchor by the binary
+					// digits of its index: lane i gets sequence i's position
+					uint32_t jt[PC_ANCH + 1];
+					jt[0] = pk;
+#pragma unroll
+					for (int r = 1; r <= PC_ANCH; ++r) {
+						uint32_t j = 0;
+#pragma unroll
+						for (int q = 0; q < WIN / 64; ++q)
+							j |= win_next(jt[r - 1], (jt[r - 1] >> (8 * q)) & 0xffu) << (8 * q);
+						jt[r] = j;
+					}
+					const int32_t wl = uni(MAXTOK - nb < 64 ? MAXTOK - nb : 64);
+					uint32_t cj = 0xffffu;
+					int32_t cur = 0, walked = 0;
+					do {
+						cj = ((lane >> PC_ANCH) == walked) ? uint32_t(cur) : cj;
+						++walked;
+						const uint32_t w =
+						    uint32_t(__builtin_amdgcn_readlane(int32_t(jt[PC_ANCH]), cur & 63));
+						cur = uni(int32_t((w >> (8 * (cur >> 6))) & 0xffu));
+					} while (cur != 0 && (walked << PC_ANCH) < wl);
+#pragma unroll
+					for (int r = PC_ANCH - 1; r >= 0; --r) {
+						const uint32_t x = win_look(jt[r], cj & 0xffu);
+						if ((lane >> r) & 1)
+							cj = (cj < WIN && x) ? x : 0xffffu;
+					}
+					STAMP(SP_DOUBLE);
+					const bool inwin = cj < WIN;
+					const Cand tk = (s + WIN + 2 * 272 < n)
+					                    ? parse_cand_far(L.inb, mis, s + (inwin ? int32_t(cj) : 0))
+					                    : parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
+					const int32_t kL = tk.L, klit = tk.lit, koff = tk.off, kml = tk.ml;
+					const int32_t knext = tk.next, kkind = tk.kind;
+					const bool good = inwin && (kkind == TK_NORMAL || kkind == TK_LAST);
+					const int32_t klen = kL + kml;
+					const int32_t incl = wave_incl_scan(good ? klen : 0);
+					const int32_t tstart = blen + incl - klen;
+					const int32_t d0 = o + tstart + kL;
+					const bool fits = good && lane < MAXTOK - nb && klen <= PC_BIG &&
+					                  blen + incl <= OUTB && o + blen + incl <= cap &&
+					                  (kkind != TK_NORMAL || d0 - koff >= 0) &&
+					                  (koff >= 16 || kml <= 64);
+					const uint64_t badm = __ballot(!fits);
+					const int cnt = badm ? (__ffsll((long long)badm) - 1) : 64;
+					const int32_t cnext = cnt > 0 ? __shfl(knext, cnt - 1) : s;
+					const int32_t ckind_last = cnt > 0 ? __shfl(kkind, cnt - 1) : TK_NORMAL;
+					if (lane < cnt) {
+						L.r_tstart[ps][nb + lane] = tstart;
+						L.r_L[ps][nb + lane] = kL;
+						L.r_lit[ps][nb + lane] = klit;
+						L.r_off[ps][nb + lane] = koff;
+						L.r_ml[ps][nb + lane] = kml;
+					}
+					STAMP_COUNT(SP_TOKENS, cnt);
+					smode = cnt > 0 && cnext - s_win >= PC_SER_MIN * cnt;
+					const bool was_empty = (nb == 0);
+					if (was_empty && cnt > 0)
+						bcomp0 = s;
+					nb += cnt;
+					blen += cnt > 0 ? __shfl(incl, cnt - 1) : 0;
+					if (cnt > 0 && ckind_last == TK_LAST) {
+						end_block = true;
+						s = n;
+					} else if (cnt > 0 && cnext >= n) {
+						end_block = true;  // block ends right after a match (lz4ada.adb:780)
+						s = cnext;
+					} else if (cnt > 0) {
+						s = cnext;
+					} else if (was_empty) {
+						stop = true;
+					} else {
+						force_flush = true;
 					}
 				}
+				wave_lds_fence();
+				STAMP(SP_SELECT);
+				if (end_block || stop || force_flush ||
+				    nb > (smode ? MAXTOK - 1 : MAXTOK - WTOK / 2) || blen > OUTB - PC_BIG ||
+				    (s - bcomp0) >= PC_SPAN)
+					break;
 			}
-		} else {
-			// ------------------------------------------------ consumer
-			const int c = slot ^ 1;
-			if (L.m_nb[c] > 0) {
-				pc_copy_batch(L, c, mis, ob STAMP_ARGS);
+			if (nb > 0) {
+				if (lane == 0) {
+					L.m_nb[ps] = nb;
+					L.m_blen[ps] = blen;
+					L.m_o[ps] = o;
+					L.m_bcomp0[ps] = bcomp0;
+				}
 				wave_lds_fence();
 				if (lane == 0)
-					L.m_nb[c] = 0;
+					L.full[ps] = 1;
+				o += blen;
+				++pseq;
 			}
-		}
-		STAMP(SP_WAIT);  // (wave's own work is stamped; this closes it)
-		__syncthreads();
-		if (threadIdx.x == 0)
-			L.flags = (pdone ? 1 : 0) | (pone ? 2 : 0);
-		__syncthreads();
-		STAMP(SP_WAIT);
-		int fl = L.flags;
-		const bool full = L.m_nb[0] > 0 || L.m_nb[1] > 0;
-		if ((fl & 2) && !full) {
-			// every batch is in HBM: the producer takes the one-token path
-			if (wave == 0) {
+			if (end_block)
+				pdone = true;
+			if (stop && !pdone) {
+				// every queued batch must be in HBM: the one-token path reads
+				// its history there
+				for (int k = 0; k < PC_SLOTS; ++k)
+					while (lds_poll(&L.full[k]))
+						__builtin_amdgcn_s_sleep(1);
+				STAMP(SP_WAIT);
 				int64_t s64 = s, o64 = o;
 				if (!one_token(in, n, ob, cap, s64, o64, st)) {
 					ok = false;
@@ -1697,20 +1722,36 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 					if (s >= n)
 						pdone = true;
 				}
-				pone = false;
 				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 				STAMP(SP_ONE);
 			}
-			__syncthreads();
-			if (threadIdx.x == 0)
-				L.flags = (pdone ? 1 : 0);
-			__syncthreads();
-			fl = L.flags;
 		}
-		if ((fl & 1) && !full)
-			break;
-		slot ^= 1;
+		wave_lds_fence();
+		if (lane == 0)
+			L.pdone = 1;
+	} else {
+		// ---------------------------------------------------- consumer
+		for (int32_t cseq = 0;; ++cseq) {
+			const int cs = cseq & (PC_SLOTS - 1);
+			bool have = true;
+			while (!lds_poll(&L.full[cs])) {
+				if (lds_poll(&L.pdone) && !lds_poll(&L.full[cs])) {
+					have = false;
+					break;
+				}
+				__builtin_amdgcn_s_sleep(1);
+			}
+			STAMP(SP_WAIT);
+			if (!have)
+				break;
+			asm volatile("" ::: "memory");
+			pc_copy_batch(L, cs, mis, ob STAMP_ARGS);
+			wave_lds_fence();
+			if (lane == 0)
+				L.full[cs] = 0;
+		}
 	}
+	__syncthreads();
 	STAMP_FLUSH();
 
 	if (threadIdx.x == 0) {

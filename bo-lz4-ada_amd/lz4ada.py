@@ -177,6 +177,7 @@ _sig = {
     "lz4ada_xxh32_reset": ([_P(XXH32State), ctypes.c_uint32], None),
     "lz4ada_xxh32_update": ([_P(XXH32State), _vp, _i64], ctypes.c_int),
     "lz4ada_xxh32_update_device": ([_P(XXH32State), _vp, _i64, _vp], ctypes.c_int),
+    "lz4ada_content_xxh32_d2h": ([_P(XXH32State), _vp, _i64, _vp, _vp], ctypes.c_int),
     "lz4ada_xxh32_final": ([_P(XXH32State)], ctypes.c_uint32),
     "lz4ada_xxh32_hash": ([_vp, _i64, _P(ctypes.c_uint32)], ctypes.c_int),
     "lz4ada_frame_index": ([_vp, _i64, _P(FrameInfo), _vp, _i64], ctypes.c_int),
@@ -312,6 +313,13 @@ class XXHash32:
     def update_device(self, d_ptr: int, length: int, stream: int = 0):
         _check(_lib.lz4ada_xxh32_update_device(ctypes.byref(self._s), d_ptr, length, stream),
                _thread_error())
+
+    def update_device_d2h(self, d_ptr, length, host_out=None, stream=0):
+        """Update over device bytes via the D2H + host-chain pipeline; the
+        bytes are also copied into host_out (a writable buffer) if given."""
+        _check(_lib.lz4ada_content_xxh32_d2h(ctypes.byref(self._s), d_ptr, length,
+                                             _addr(host_out) if host_out is not None else None,
+                                             stream), _thread_error())
 
     def final(self) -> int:
         return _lib.lz4ada_xxh32_final(ctypes.byref(self._s))

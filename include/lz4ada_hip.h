@@ -129,6 +129,13 @@ int lz4ada_xxh32_update(lz4ada_xxh32_state *h, const uint8_t *data, int64_t len)
 /* Same over device-resident bytes; stream is a hipStream_t (0 = default). */
 int lz4ada_xxh32_update_device(lz4ada_xxh32_state *h, const void *d_data, int64_t len,
                                void *stream);
+/* Content checksum pipeline: XXHash32.Update over
+ * device-resident bytes copied to the host in 32 MiB chunks, each chunk
+ * hashed on the calling host thread while the next one is in flight; the
+ * bytes also land in host_out when it is not NULL.  The serial chain runs
+ * ~5x faster on a host core than on one GPU wave. */
+int lz4ada_content_xxh32_d2h(lz4ada_xxh32_state *h, const void *d_data, int64_t len,
+                             uint8_t *host_out, void *stream);
 /* XXHash32.Final (lz4ada.adb:993-1017). */
 uint32_t lz4ada_xxh32_final(const lz4ada_xxh32_state *h);
 /* XXHash32.Hash (lz4ada.adb:1019-1024), seed 0, host bytes. */

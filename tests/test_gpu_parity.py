@@ -90,6 +90,31 @@ def test_xxh32_random_against_oracle():
     assert h.final() == O.xxh32(data)
 
 
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 1000, (32 << 20) - 3, (32 << 20) + 16 + 5,
+                               (64 << 20) + 9])
+def test_content_checksum_pipeline(n):
+    """lz4ada_content_xxh32_d2h (D2H + host chain) equals the oracle's XXH32
+    and delivers the bytes; its state continues the GPU chain's and back."""
+    import torch
+    g = torch.Generator().manual_seed(n)
+    host = torch.randint(0, 256, (n + 64,), dtype=torch.uint8, generator=g)
+    d = host.cuda()
+    data = bytes(host[:n].numpy())
+    want = O.xxh32(data)
+    h = lz4ada.XXHash32()
+    out = bytearray(n)
+    h.update_device_d2h(d.data_ptr(), n, out)
+    assert h.final() == want
+    assert bytes(out) == data
+    # split: GPU chain for an odd prefix, host pipeline for the rest, and back
+    k = n // 3 + 1 if n else 0
+    h = lz4ada.XXHash32()
+    h.update_device(d.data_ptr(), k)
+    h.update_device_d2h(d.data_ptr() + k, max(n - k - 5, 0))
+    h.update_device(d.data_ptr() + k + max(n - k - 5, 0), n - k - max(n - k - 5, 0))
+    assert h.final() == want
+
+
 def test_decompress_individual_bytes():
     # lz4test.adb:149-214
     tc = bytes.fromhex(
