@@ -285,6 +285,67 @@ static bool is_any_magic(uint32_t v)
 	return v == MAGIC_MODERN || v == MAGIC_LEGACY || (v >= MAGIC_SKIP_LO && v <= MAGIC_SKIP_HI);
 }
 
+// XXHash32.Update / Final (lz4ada.adb:942-1017) on host bytes the GPU
+// decoded (content checksums: the facade's Hash_All_Data and the bulk
+// path's pipeline).  The state layout is the one the GPU kernel
+// k_xxh32_update advances, so the two can continue each other.
+static inline uint32_t rotl32h(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static inline uint32_t xxh_round(uint32_t acc, uint32_t w) { return rotl32h(acc + w * P2, 13) * P1; }
+
+static void host_xxh32_update(lz4ada_xxh32_state& h, const uint8_t* p, size_t n)
+{
+	h.total_length += n;
+	size_t bs = size_t(h.buffer_size);
+	if (bs + n < 16) {
+		if (n)
+			memcpy(h.buffer + bs, p, n);
+		h.buffer_size = int32_t(bs + n);
+		return;
+	}
+	if (bs) {  // complete the buffered stripe (Update1, :965-991)
+		const size_t k = 16 - bs;
+		memcpy(h.buffer + bs, p, k);
+		p += k;
+		n -= k;
+		for (int i = 0; i < 4; ++i)
+			h.state[i] = xxh_round(h.state[i], load32(h.buffer + 4 * i));
+	}
+	uint32_t v0 = h.state[0], v1 = h.state[1], v2 = h.state[2], v3 = h.state[3];
+	for (; n >= 16; p += 16, n -= 16) {  // stripes (Process, :951-958)
+		v0 = xxh_round(v0, load32(p));
+		v1 = xxh_round(v1, load32(p + 4));
+		v2 = xxh_round(v2, load32(p + 8));
+		v3 = xxh_round(v3, load32(p + 12));
+	}
+	h.state[0] = v0;
+	h.state[1] = v1;
+	h.state[2] = v2;
+	h.state[3] = v3;
+	if (n)
+		memcpy(h.buffer, p, n);
+	h.buffer_size = int32_t(n);
+}
+
+static uint32_t host_xxh32_final(const lz4ada_xxh32_state& h)  // :993-1017
+{
+	uint32_t acc = h.total_length >= 16 ? rotl32h(h.state[0], 1) + rotl32h(h.state[1], 7) +
+	                                          rotl32h(h.state[2], 12) + rotl32h(h.state[3], 18)
+	                                    : h.state[2] + P5;
+	acc += uint32_t(h.total_length);
+	const uint8_t* p = h.buffer;
+	size_t n = size_t(h.buffer_size);
+	for (; n >= 4; p += 4, n -= 4)
+		acc = rotl32h(acc + load32(p) * P3, 17) * P4;
+	for (; n; ++p, --n)
+		acc = rotl32h(acc + uint32_t(*p) * P5, 11) * P1;
+	acc ^= acc >> 15;
+	acc *= P2;
+	acc ^= acc >> 13;
+	acc *= P3;
+	acc ^= acc >> 16;
+	return acc;
+}
+
 // Device status of a decode kernel -> the reference's exception.
 [[noreturn]] static void raise_device_status(const SerialState& s)
 {
@@ -337,10 +398,33 @@ struct lz4ada_decompressor {
 	DevBuf<uint8_t> d_buf;  // mirror of the caller's Buffer (history lives here)
 	int64_t d_buf_len = 0;
 	DevBuf<uint8_t> d_blk;
-	DevBuf<lz4ada_xxh32_state> d_hash;  // Hash_All_Data
+	lz4ada_xxh32_state hash_all{};  // Hash_All_Data, over the bytes the GPU decoded
 	DevBuf<lz4ada_xxh32_state> d_tmp_hash;
 	DevBuf<SerialState> d_serial;
+	DevBuf<lz4ada_block_desc> d_desc;  // one-block fast path
+	DevBuf<lz4ada_block_status> d_bst;
 
+	// Read-ahead: when one Update call hands over several
+	// complete blocks, they are decoded together by the bulk decoder and
+	// then served one per call, as the reference returns them.
+	struct Ahead {
+		std::vector<uint8_t> input;  // the batch's compressed bytes (identity check)
+		std::vector<lz4ada_block_desc> descs;
+		std::vector<lz4ada_block_status> st;
+		DevBuf<uint8_t> d_in, d_out;
+		DevBuf<lz4ada_block_desc> d_desc;
+		DevBuf<lz4ada_block_status> d_st;
+		uint64_t slot = 0;
+		size_t next = 0;  // next block to serve
+		void clear()
+		{
+			descs.clear();
+			st.clear();
+			next = 0;
+		}
+	} ahead;
+
+	lz4ada_decompressor() { lz4ada_xxh32_reset(&hash_all, 0); }
 	~lz4ada_decompressor()
 	{
 		if (stream) {
@@ -356,25 +440,19 @@ struct lz4ada_decompressor {
 		device_check_or_raise();
 		HIP_OK(hipGetDevice(&device));
 		HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-		d_hash.reserve(1);
 		d_tmp_hash.reserve(1);
 		d_serial.reserve(1);
+		d_desc.reserve(1);
+		d_bst.reserve(1);
 		dev_ready = true;
-		reset_content_hash();
 	}
 
-	void reset_content_hash()  // XXHash32.Reset(0) on the device state
-	{
-		if (!dev_ready)
-			return;
-		lz4ada_xxh32_state h;
-		lz4ada_xxh32_reset(&h, 0);
-		HIP_OK(hipMemcpyAsync(d_hash.p, &h, sizeof h, hipMemcpyHostToDevice, stream));
-	}
+	void reset_content_hash() { lz4ada_xxh32_reset(&hash_all, 0); }  // XXHash32.Reset(0)
 
 	// ---------------------------------------------------- Update pieces
 	void reset_outer()  // lz4ada.adb:451-461
 	{
+		ahead.clear();
 		is_at_end_mark = false;
 		input_length = -1;
 		output_pos = 0;
@@ -416,16 +494,7 @@ struct lz4ada_decompressor {
 			              img_u(m.size_remaining) + " bytes left to output.");
 	}
 
-	uint32_t content_hash_final()
-	{
-		ensure_device();
-		// refresh the cached Final() on the device (len = 0 update)
-		HIP_OK(launch_xxh32_update(d_hash.p, nullptr, 0, stream));
-		lz4ada_xxh32_state h;
-		HIP_OK(hipMemcpyAsync(&h, d_hash.p, sizeof h, hipMemcpyDeviceToHost, stream));
-		HIP_OK(hipStreamSynchronize(stream));
-		return h.hash;
-	}
+	uint32_t content_hash_final() { return host_xxh32_final(hash_all); }
 
 	void check_end_mark(const uint8_t* in, int64_t len, int64_t& consumed)  // :463-523
 	{
@@ -495,6 +564,20 @@ struct lz4ada_decompressor {
 		return n;
 	}
 
+	void grow_mirror(int64_t buflen)  // the Buffer mirror, keeping history
+	{
+		DevBuf<uint8_t> nb;
+		nb.reserve(size_t(buflen));
+		HIP_OK(hipMemsetAsync(nb.p, 0, size_t(buflen), stream));
+		if (d_buf_len)
+			HIP_OK(hipMemcpyAsync(nb.p, d_buf.p, size_t(d_buf_len), hipMemcpyDeviceToDevice,
+			                      stream));
+		HIP_OK(hipStreamSynchronize(stream));
+		std::swap(nb.p, d_buf.p);
+		std::swap(nb.n, d_buf.n);
+		d_buf_len = buflen;
+	}
+
 	// Decode_Full_Block_With_Trailer (lz4ada.adb:661-714) on the GPU.
 	void decode_full_block(const uint8_t* blk, int64_t blen, uint8_t* buf, int64_t buflen,
 	                       int64_t& first, int64_t& last)
@@ -502,18 +585,8 @@ struct lz4ada_decompressor {
 		ensure_device();
 		const int bcl = m.block_checksum_length;
 		const int64_t raw_len = blen - bcl;
-		if (buflen > d_buf_len) {  // grow the Buffer mirror, keeping history
-			DevBuf<uint8_t> nb;
-			nb.reserve(size_t(buflen));
-			HIP_OK(hipMemsetAsync(nb.p, 0, size_t(buflen), stream));
-			if (d_buf_len)
-				HIP_OK(hipMemcpyAsync(nb.p, d_buf.p, size_t(d_buf_len), hipMemcpyDeviceToDevice,
-				                      stream));
-			HIP_OK(hipStreamSynchronize(stream));
-			std::swap(nb.p, d_buf.p);
-			std::swap(nb.n, d_buf.n);
-			d_buf_len = buflen;
-		}
+		if (buflen > d_buf_len)
+			grow_mirror(buflen);
 		d_blk.reserve(size_t(std::max<int64_t>(blen, 1)));
 		if (blen > 0)
 			HIP_OK(hipMemcpyAsync(d_blk.p, blk, size_t(blen), hipMemcpyHostToDevice, stream));
@@ -529,6 +602,10 @@ struct lz4ada_decompressor {
 				raise(LZ4ADA_CHECKSUM_ERROR, "Declared checksum is 0x" + hex32(expect) +
 				                                     ", but computed one is 0x" + hex32(h.hash) +
 				                                     ".");
+		}
+		if (try_fast_block(raw_len, blen, buflen, first, last)) {
+			deliver(buf, first, last);
+			return;
 		}
 		SerialState s{};
 		s.output_pos = output_pos;
@@ -550,14 +627,201 @@ struct lz4ada_decompressor {
 			raise_device_status(s);
 		first = s.first;
 		last = s.last;
+		deliver(buf, first, last);
+	}
+
+	// The block's output, in the Buffer mirror at [first, last], to the
+	// caller's Buffer, and into the content checksum (Update_Checksum,
+	// :709-714) on the way.
+	void deliver(uint8_t* buf, int64_t first, int64_t last)
+	{
 		const int64_t nout = last - first + 1;
-		if (nout > 0) {
-			if (m.content_checksum_length != 0)  // Update_Checksum (:709-714)
-				HIP_OK(launch_xxh32_update(d_hash.p, d_buf.p + first, uint64_t(nout), stream));
-			HIP_OK(hipMemcpyAsync(buf + first, d_buf.p + first, size_t(nout),
-			                      hipMemcpyDeviceToHost, stream));
-			HIP_OK(hipStreamSynchronize(stream));
+		if (nout <= 0)
+			return;
+		HIP_OK(hipMemcpyAsync(buf + first, d_buf.p + first, size_t(nout), hipMemcpyDeviceToHost,
+		                      stream));
+		HIP_OK(hipStreamSynchronize(stream));
+		if (m.content_checksum_length != 0)
+			host_xxh32_update(hash_all, buf + first, size_t(nout));
+	}
+
+	// A lone block is latency-bound: the 512-lane workgroup decoder (blocks
+	// it declines are redone by the one-wave decoder) decodes a 4 MiB block
+	// ~1.6x sooner than the two-wave decoder (tools/facade_time.py).
+	static int facade_variant()
+	{
+		const char* e = getenv("LZ4ADA_FACADE_DECODER");
+		if (e && !strcmp(e, "wave"))
+			return DEC_WAVE;
+		if (e && !strcmp(e, "pc"))
+			return DEC_PC;
+		return DEC_WG;
+	}
+
+	// Decompress_Full_Block through the bulk decoder for one block: the
+	// block's output goes to the Buffer mirror at the position the reference
+	// would use.  Any status but OK -- including a reference before the
+	// block start, which only the exact path resolves (history scheme,
+	// D1) -- or a content-size overrun leaves the block to k_serial_block,
+	// which redoes it from the same state; the bulk decoder stops at the
+	// first such sequence, so the history that re-run reads is untouched.
+	bool try_fast_block(int64_t raw_len, int64_t blen, int64_t buflen, int64_t& first,
+	                    int64_t& last)
+	{
+		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
+		if (linked || getenv("LZ4ADA_FACADE_EXACT"))
+			return false;
+		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;  // :678-680
+		const int64_t cap = std::min<int64_t>(buflen - start, INT32_MAX);
+		if (cap <= 0 || raw_len > INT32_MAX)
+			return false;
+		lz4ada_block_desc d{};
+		d.in_off = 0;
+		d.in_len = uint32_t(raw_len);
+		d.flags = m.is_compressed ? 0u : LZ4ADA_BLOCK_STORED;
+		d.out_off = uint64_t(start);
+		d.out_cap = uint32_t(cap);
+		HIP_OK(hipMemcpyAsync(d_desc.p, &d, sizeof d, hipMemcpyHostToDevice, stream));
+		HIP_OK(launch_decode_variant(d_blk.p, uint64_t(std::max<int64_t>(blen, 1)), d_desc.p, 1,
+		                             d_buf.p, d_bst.p, facade_variant(), stream));
+		lz4ada_block_status st;
+		HIP_OK(hipMemcpyAsync(&st, d_bst.p, sizeof st, hipMemcpyDeviceToHost, stream));
+		HIP_OK(hipStreamSynchronize(stream));
+		if (st.code != DS_OK)
+			return false;
+		const int64_t nout = int64_t(st.out_len);
+		if (m.has_content_size && uint64_t(nout) > m.size_remaining)
+			return false;  // the exact path raises mid-block, as the reference does
+		if (m.has_content_size)
+			m.size_remaining -= uint64_t(nout);
+		output_pos = start + nout;
+		if (output_pos >= HISTORY_SIZE)  // :785-787 (:688-690 for stored blocks)
+			output_pos_history = output_pos;
+		first = start;
+		last = start + nout - 1;
+		return true;
+	}
+
+	// Decode the current block (payload at blk, `total` bytes with its
+	// checksum) and every complete block after it in [blk, end), up to the
+	// end mark, in one bulk launch.  False when fewer than two are there.
+	bool build_ahead(const uint8_t* blk, int64_t total, const uint8_t* end, int64_t buflen)
+	{
+		ahead.clear();
+		if (m.is_format != F_MODERN && m.is_format != F_LEGACY)
+			return false;
+		if (m.is_format == F_MODERN && !(m.flg & 0x20u))
+			return false;  // linked frame: every block needs the history (exact path)
+		const int bcl = m.block_checksum_length;
+		const int64_t avail = end - blk;
+		const uint64_t slot = (uint64_t(std::min<int64_t>(buflen, INT32_MAX)) + 255) & ~uint64_t(255);
+		const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(2) << 30) / slot);
+		auto add = [&](int64_t off, int64_t sz, bool stored) {
+			lz4ada_block_desc d{};
+			d.in_off = uint64_t(off);
+			d.in_len = uint32_t(sz);
+			d.flags = (stored ? LZ4ADA_BLOCK_STORED : 0u) | (bcl ? LZ4ADA_BLOCK_HAS_CKSUM : 0u);
+			d.out_off = uint64_t(ahead.descs.size()) * slot;
+			d.out_cap = uint32_t(std::min<int64_t>(buflen, INT32_MAX));
+			d.cksum = bcl ? load32(blk + off + sz) : 0u;
+			ahead.descs.push_back(d);
+		};
+		add(0, total - bcl, !m.is_compressed);
+		int64_t pos = total;
+		while (pos + BLOCK_SIZE_BYTES <= avail && ahead.descs.size() < max_blocks &&
+		       pos < (int64_t(512) << 20)) {
+			uint32_t w = load32(blk + pos);
+			bool stored = false;
+			if (m.is_format == F_MODERN) {
+				if (w == 0)
+					break;  // end mark
+				stored = (w & 0x80000000u) != 0;
+				w &= 0x7ffffffu;
+			} else if (is_any_magic(w)) {
+				break;  // the next frame
+			}
+			const int64_t sz = int64_t(w);
+			if (sz + BLOCK_SIZE_BYTES + bcl > int64_t(input_buffer.size()) ||
+			    pos + BLOCK_SIZE_BYTES + sz + bcl > avail)
+				break;  // the exact path reports it, or the rest comes later
+			add(pos + BLOCK_SIZE_BYTES, sz, stored);
+			pos += BLOCK_SIZE_BYTES + sz + bcl;
 		}
+		const size_t nb = ahead.descs.size();
+		if (nb < 2) {
+			ahead.clear();
+			return false;
+		}
+		ahead.input.assign(blk, blk + pos);
+		ahead.slot = slot;
+		ahead.st.assign(nb, lz4ada_block_status{});
+		ahead.d_in.reserve(size_t(pos));
+		ahead.d_out.reserve(size_t(nb * slot));
+		ahead.d_desc.reserve(nb);
+		ahead.d_st.reserve(nb);
+		HIP_OK(hipMemcpyAsync(ahead.d_in.p, blk, size_t(pos), hipMemcpyHostToDevice, stream));
+		HIP_OK(hipMemcpyAsync(ahead.d_desc.p, ahead.descs.data(), nb * sizeof(lz4ada_block_desc),
+		                      hipMemcpyHostToDevice, stream));
+		HIP_OK(hipMemsetAsync(ahead.d_st.p, 0, nb * sizeof(lz4ada_block_status), stream));
+		if (bcl)
+			HIP_OK(launch_block_checksums(ahead.d_in.p, ahead.d_desc.p, uint32_t(nb), ahead.d_st.p,
+			                              stream));
+		HIP_OK(launch_decode_variant(ahead.d_in.p, uint64_t(pos), ahead.d_desc.p, uint32_t(nb),
+		                             ahead.d_out.p, ahead.d_st.p, DEC_PC, stream));
+		HIP_OK(hipMemcpyAsync(ahead.st.data(), ahead.d_st.p, nb * sizeof(lz4ada_block_status),
+		                      hipMemcpyDeviceToHost, stream));
+		HIP_OK(hipStreamSynchronize(stream));
+		return true;
+	}
+
+	// Serve the current block from the read-ahead batch when it is the
+	// batch's next block (same bytes) and decoded cleanly; the state moves
+	// exactly as Decode_Full_Block_With_Trailer would move it.
+	bool serve_ahead(const uint8_t* blk, int64_t total, const uint8_t* end, uint8_t* buf,
+	                 int64_t buflen, int64_t& first, int64_t& last)
+	{
+		if (getenv("LZ4ADA_FACADE_EXACT"))
+			return false;
+		ensure_device();
+		const int bcl = m.block_checksum_length;
+		auto same = [&](size_t k) {
+			const lz4ada_block_desc& d = ahead.descs[k];
+			return int64_t(d.in_len) + bcl == total &&
+			       memcmp(ahead.input.data() + d.in_off, blk, size_t(total)) == 0;
+		};
+		if (ahead.next >= ahead.descs.size() || !same(ahead.next)) {
+			if (!build_ahead(blk, total, end, buflen))
+				return false;
+		}
+		const size_t k = ahead.next++;
+		const lz4ada_block_desc& d = ahead.descs[k];
+		const lz4ada_block_status& st = ahead.st[k];
+		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;  // :678-680
+		const int64_t nout = int64_t(st.out_len);
+		if (st.code != DS_OK || (bcl && st.cksum != d.cksum) || start + nout > buflen ||
+		    (m.has_content_size && uint64_t(nout) > m.size_remaining)) {
+			ahead.clear();  // the exact path takes this block (and reports it)
+			return false;
+		}
+		if (buflen > d_buf_len)
+			grow_mirror(buflen);
+		const uint8_t* src = ahead.d_out.p + d.out_off;
+		if (nout > 0) {  // the mirror keeps the history for a later exact block
+			HIP_OK(hipMemcpyAsync(d_buf.p + start, src, size_t(nout), hipMemcpyDeviceToDevice,
+			                      stream));
+			HIP_OK(hipMemcpyAsync(buf + start, src, size_t(nout), hipMemcpyDeviceToHost, stream));
+			HIP_OK(hipStreamSynchronize(stream));
+			if (m.content_checksum_length != 0)
+				host_xxh32_update(hash_all, buf + start, size_t(nout));
+		}
+		if (m.has_content_size)
+			m.size_remaining -= uint64_t(nout);
+		output_pos = start + nout;
+		if (output_pos >= HISTORY_SIZE)
+			output_pos_history = output_pos;
+		first = start;
+		last = start + nout - 1;
+		return true;
 	}
 
 	void cache_and_process(const uint8_t* in, int64_t len, int64_t& consumed, uint8_t* buf,
@@ -614,7 +878,8 @@ struct lz4ada_decompressor {
 					consumed += total;
 					m.input_buffer_filled = 0;
 					input_length = -1;
-					decode_full_block(blk, total, buf, buflen, first, last);
+					if (!serve_ahead(blk, total, in + len, buf, buflen, first, last))
+						decode_full_block(blk, total, buf, buflen, first, last);
 				} else {
 					cache_and_process(in, len, consumed, buf, buflen, first, last);
 				}
@@ -653,66 +918,6 @@ static int guarded(std::string* err, F&& f)
 		g_thread_error = "out of host memory";
 		return LZ4ADA_CONSTRAINT_ERROR;
 	}
-}
-
-// XXHash32.Update / Final (lz4ada.adb:942-1017) on host bytes, for the
-// content checksum pipeline only; the state layout is the one the GPU
-// kernel k_xxh32_update advances, so the two can continue each other.
-static inline uint32_t rotl32h(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-static inline uint32_t xxh_round(uint32_t acc, uint32_t w) { return rotl32h(acc + w * P2, 13) * P1; }
-
-static void host_xxh32_update(lz4ada_xxh32_state& h, const uint8_t* p, size_t n)
-{
-	h.total_length += n;
-	size_t bs = size_t(h.buffer_size);
-	if (bs + n < 16) {
-		if (n)
-			memcpy(h.buffer + bs, p, n);
-		h.buffer_size = int32_t(bs + n);
-		return;
-	}
-	if (bs) {  // complete the buffered stripe (Update1, :965-991)
-		const size_t k = 16 - bs;
-		memcpy(h.buffer + bs, p, k);
-		p += k;
-		n -= k;
-		for (int i = 0; i < 4; ++i)
-			h.state[i] = xxh_round(h.state[i], load32(h.buffer + 4 * i));
-	}
-	uint32_t v0 = h.state[0], v1 = h.state[1], v2 = h.state[2], v3 = h.state[3];
-	for (; n >= 16; p += 16, n -= 16) {  // stripes (Process, :951-958)
-		v0 = xxh_round(v0, load32(p));
-		v1 = xxh_round(v1, load32(p + 4));
-		v2 = xxh_round(v2, load32(p + 8));
-		v3 = xxh_round(v3, load32(p + 12));
-	}
-	h.state[0] = v0;
-	h.state[1] = v1;
-	h.state[2] = v2;
-	h.state[3] = v3;
-	if (n)
-		memcpy(h.buffer, p, n);
-	h.buffer_size = int32_t(n);
-}
-
-static uint32_t host_xxh32_final(const lz4ada_xxh32_state& h)  // :993-1017
-{
-	uint32_t acc = h.total_length >= 16 ? rotl32h(h.state[0], 1) + rotl32h(h.state[1], 7) +
-	                                          rotl32h(h.state[2], 12) + rotl32h(h.state[3], 18)
-	                                    : h.state[2] + P5;
-	acc += uint32_t(h.total_length);
-	const uint8_t* p = h.buffer;
-	size_t n = size_t(h.buffer_size);
-	for (; n >= 4; p += 4, n -= 4)
-		acc = rotl32h(acc + load32(p) * P3, 17) * P4;
-	for (; n; ++p, --n)
-		acc = rotl32h(acc + uint32_t(*p) * P5, 11) * P1;
-	acc ^= acc >> 15;
-	acc *= P2;
-	acc ^= acc >> 13;
-	acc *= P3;
-	acc ^= acc >> 16;
-	return acc;
 }
 
 static lz4ada_decompressor* new_ctx(int64_t in_last)

@@ -1,0 +1,182 @@
+"""The streaming facade (Init_With_Header + Update, lz4ada.adb:383-659) over
+its GPU paths -- the one-block bulk decode and the read-ahead batch -- traced
+call by call against the oracle's facade: Num_Consumed, Output_First/Last,
+the delivered bytes, End_Of_Frame and the exception text must be identical
+(tool_unlz4ada's loop, unlz4ada.adb:84-103, at several input feed sizes)."""
+import ctypes
+import random
+
+import pytest
+
+import _oracle as O
+
+import lz4ada
+import lz4frame
+
+pytestmark = pytest.mark.gpu
+
+KiB = 1024
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not lz4ada.device_available():
+        pytest.fail("MI355X not usable: " + lz4ada._thread_error())
+
+
+def trace_ours(frame, feed, reservation=lz4ada.Reservation.Single_Frame):
+    tr = []
+    try:
+        ctx, pos, mbs = lz4ada.Decompressor.init_with_header(frame, reservation)
+    except lz4ada.LZ4AdaError as e:
+        return [("init", str(e))]
+    buf = bytearray(mbs)
+    while pos < len(frame):
+        stop = len(frame) if feed == 0 else min(len(frame), pos + feed)
+        try:
+            c, f, l = ctx.update(frame, buf, pos, stop)
+        except lz4ada.LZ4AdaError as e:
+            tr.append(("error", str(e)))
+            return tr
+        tr.append((c, f, l, bytes(buf[f:l + 1]) if l >= f else b"", int(ctx.is_end_of_frame())))
+        pos += c
+        if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
+            break
+    return tr
+
+
+def trace_oracle(frame, feed, reservation=O.SINGLE_FRAME):
+    tr = []
+    st, msg, ctx, pos = O.Decompressor.init_with_header(frame, reservation)
+    if st:
+        return [("init", O.exception_information(st, msg))]
+    buf = ctypes.create_string_buffer(ctx.min_buffer_size)
+    while pos < len(frame):
+        stop = len(frame) if feed == 0 else min(len(frame), pos + feed)
+        st, c, f, l = ctx.update(frame[pos:stop], buf)
+        if st:
+            tr.append(("error", O.exception_information(st, ctx.last_error())))
+            return tr
+        tr.append((c, f, l, buf.raw[f:l + 1] if l >= f else b"", ctx.is_end_of_frame()))
+        pos += c
+        if ctx.is_end_of_frame() == O.EOF_YES:
+            break
+    return tr
+
+
+def synth(kinds, nblocks, block_max, seed, stored_every=0, **kw):
+    blocks = []
+    for i in range(nblocks):
+        n = block_max if i < nblocks - 1 else block_max // 3 + 11
+        if stored_every and i % stored_every == stored_every - 1:
+            raw = random.Random(seed + i).randbytes(n)
+            blocks.append((raw, raw, True))
+        else:
+            comp, raw = lz4ada.gen_block(kinds[i % len(kinds)], seed * 100 + i, n)
+            blocks.append((comp, raw, False))
+    return lz4frame.build_frame(blocks, block_max, **kw)
+
+
+def same_trace(frame, feed):
+    ours, ref = trace_ours(frame, feed), trace_oracle(frame, feed)
+    assert len(ours) == len(ref)
+    for k, (a, b) in enumerate(zip(ours, ref)):
+        assert a == b, f"call {k}: {a[:3] if len(a) > 3 else a} != {b[:3] if len(b) > 3 else b}"
+    return ours
+
+
+@pytest.mark.parametrize("feed", [0, 300_000, 4096])
+@pytest.mark.parametrize("kinds", [(1,), (0, 1, 2, 3)], ids=["mixed", "all"])
+def test_facade_indep_frame_trace(kinds, feed):
+    frame, raw = synth(kinds, 12, 64 * KiB, seed=11, stored_every=5, indep=True,
+                       block_cksum=True, content_cksum=True, with_content_size=True)
+    tr = same_trace(frame, feed)
+    assert b"".join(t[3] for t in tr if len(t) == 5) == raw
+
+
+@pytest.mark.parametrize("feed", [0, 1 << 20])
+def test_facade_4m_blocks_trace(feed):
+    frame, raw = synth((1, 0), 3, 4 << 20, seed=3, indep=True, block_cksum=True,
+                       content_cksum=True)
+    tr = same_trace(frame, feed)
+    assert b"".join(t[3] for t in tr if len(t) == 5) == raw
+
+
+@pytest.mark.parametrize("feed", [0, 100_000])
+def test_facade_checksum_error_midway(feed):
+    frame, raw = synth((1, 3), 10, 64 * KiB, seed=5, indep=True, block_cksum=True,
+                       content_cksum=True)
+    info, descs = lz4ada.frame_index(frame)
+    bad = bytearray(frame)
+    bad[descs[6].in_off + 10] ^= 0x21
+    tr = same_trace(bytes(bad), feed)
+    assert tr[-1][0] == "error" and "CHECKSUM_ERROR" in tr[-1][1]
+
+
+@pytest.mark.parametrize("feed", [0, 100_000])
+def test_facade_content_size_short(feed):
+    blocks = [lz4ada.gen_block(1, 40 + i, 64 * KiB) + (False,) for i in range(5)]
+    frame, raw = lz4frame.build_frame(blocks, 64 * KiB, indep=True, with_content_size=True)
+    # declare a content size smaller than the frame's output -> raised mid-block
+    hdr = bytearray(lz4frame.header(64 * KiB, True, False, False, len(raw) - 70_000))
+    body = frame[len(lz4frame.header(64 * KiB, True, False, False, len(raw))):]
+    tr = same_trace(bytes(hdr) + body, feed)
+    assert tr[-1][0] == "error"
+
+
+def split_at_sequence(comp, want):
+    """Split an LZ4 block at the first sequence boundary at or after `want`
+    compressed bytes -> (first payload, its decoded length, rest)."""
+    i = out = 0
+    while i < len(comp):
+        if i >= want:
+            return comp[:i], out, comp[i:]
+        tk = comp[i]
+        i += 1
+        lit = tk >> 4
+        if lit == 15:
+            while True:
+                b = comp[i]
+                i += 1
+                lit += b
+                if b != 255:
+                    break
+        i += lit
+        out += lit
+        if i >= len(comp):
+            break
+        i += 2
+        ml = tk & 15
+        if ml == 15:
+            while True:
+                b = comp[i]
+                i += 1
+                ml += b
+                if b != 255:
+                    break
+        out += ml + 4
+    raise AssertionError("no split point")
+
+
+@pytest.mark.parametrize("feed", [0, 50_000])
+def test_facade_d2_indep_flag_with_cross_block_refs(feed):
+    """D2: B.Indep is ignored by the reference, so an 'independent' frame
+    whose second block references the first decodes there; the read-ahead
+    batch flags the reference and the exact path resolves it."""
+    comp, raw = lz4ada.gen_block(1, 99, 200 * KiB)
+    p1, n1, p2 = split_at_sequence(comp, len(comp) // 2)
+    comp3, raw3 = lz4ada.gen_block(0, 7, 50 * KiB)
+    blocks = [(p1, raw[:n1], False), (p2, raw[n1:], False), (comp3, raw3, False)]
+    frame, whole = lz4frame.build_frame(blocks, 256 * KiB, indep=True, block_cksum=True,
+                                        content_cksum=True)
+    tr = same_trace(frame, feed)
+    assert b"".join(t[3] for t in tr if len(t) == 5) == whole
+
+
+def test_facade_legacy_readahead():
+    from conftest import read_vector
+    for name in ("z100legacy", "concatlegacy", "z101legacyplus", "minilegacy"):
+        data = read_vector(name, "lz4")
+        for feed in (0, 4096):
+            assert trace_ours(data, feed, lz4ada.FOR_ALL) == \
+                trace_oracle(data, feed, O.FOR_ALL), (name, feed)

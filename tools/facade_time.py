@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Streaming-facade (Init_With_Header + Update loop) throughput on a
+synthetic frame, the way tool_unlz4ada drives the library
+(unlz4ada.adb:84-103): the input handed over in `--feed`-byte pieces
+(0 = all remaining input per call).  Output is checked."""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bo-lz4-ada_amd"))
+
+import lz4ada  # noqa: E402
+import lz4frame  # noqa: E402
+
+
+def run(frame, expect, feed):
+    ctx, used, mbs = lz4ada.Decompressor.init_with_header(frame)
+    buf = bytearray(mbs)
+    out = bytearray()
+    pos = used
+    t0 = time.perf_counter()
+    while pos < len(frame):
+        stop = len(frame) if feed == 0 else min(len(frame), pos + feed)
+        c, f, l = ctx.update(frame, buf, pos, stop)
+        if l >= f:
+            out += buf[f:l + 1]
+        pos += c
+        if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
+            break
+    dt = time.perf_counter() - t0
+    assert bytes(out) == expect
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kind", default="mixed")
+    ap.add_argument("--blocks", type=int, default=16)
+    ap.add_argument("--block-max", type=int, default=4 << 20)
+    ap.add_argument("--feed", type=int, default=0)
+    ap.add_argument("--indep", type=int, default=1)
+    args = ap.parse_args()
+    blocks = []
+    for i in range(args.blocks):
+        comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[args.kind], 0x4C5A3441 + i, args.block_max)
+        blocks.append((comp, raw, False))
+    frame, expect = lz4frame.build_frame(blocks, args.block_max, indep=bool(args.indep),
+                                         block_cksum=True, content_cksum=True)
+    run(frame, expect, args.feed)  # warm
+    dt = run(frame, expect, args.feed)
+    print(f"facade {args.kind} feed={args.feed} {args.blocks}x{args.block_max >> 10} KiB: "
+          f"{dt * 1e3:.1f} ms  {len(expect) / dt / 2**20:.1f} MiB/s")
+
+
+if __name__ == "__main__":
+    main()
