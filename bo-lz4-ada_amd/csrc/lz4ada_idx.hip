@@ -1,0 +1,1079 @@
+// lz4ada_idx.hip -- index-driven bulk decoder for independent blocks.
+//
+// Replaces the same reference path as k_decode_pc (lib/lz4ada.adb:716-904:
+// Decompress_Full_Block / Decompress_Sequence / Write_Output /
+// Output_With_History) with two passes that keep every lane busy instead of
+// parsing one sequence chain per wave:
+//
+//  * k_index (pass 1, one wave per block).  The compressed payload is cut
+//    into 256-byte segments, 64 per 16 KiB LDS-staged chunk, one per lane.
+//    Every lane walks the sequence chain of its segment from a guessed
+//    entry (its segment start; lane 0 from the exact entry carried from the
+//    previous chunk), then each lane re-walks from the exit of the lane
+//    before it, until no entry changes.  LZ4 chains started at a wrong byte
+//    merge with the true chain within a few sequences, so this converges in
+//    2-4 walks per segment.  The walk records, for every 32-byte
+//    sub-segment, where the first sequence starting inside it begins
+//    (1 byte; 0xFF = none).  Any malformed sequence marks the block
+//    DS_RETRY.
+//  * k_decode_idx (pass 2, one wave per block).  Batches of 64 sub-segments
+//    (2 KiB of input): lane i walks the sequences starting in sub-segment i
+//    from its index entry (LDS-staged input), a wave prefix sum places them
+//    in the output, literals and matches whose source lies before the batch
+//    are copied at once, lane-parallel, straight to HBM; long runs and
+//    matches reading this batch's own output follow in output order
+//    (a leader loop: the first pending item always runs, every other whose
+//    source is already final runs with it).
+//
+// Blocks either pass declines (DS_RETRY: malformed data, a back-reference
+// before the block start, an oversize block) are redone by k_decode_pc,
+// which produces the exact statuses; so this pair never changes a result,
+// only the speed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lz4ada_internal.h"
+#include "lz4ada_dev.h"
+
+namespace lz4ada {
+namespace idx {
+
+constexpr int SEG = 256;            // pass-1 segment per lane
+constexpr int CHUNK = 64 * SEG;     // pass-1 staged chunk (16 KiB)
+constexpr int SUB = 32;             // pass-2 sub-segment per lane
+constexpr int NSUB = SEG / SUB;     // index bytes per segment
+static_assert(NSUB == 8, "one u64 of index bytes per segment");
+constexpr int BATCH = 64 * SUB;     // pass-2 batch (2 KiB of input)
+constexpr int RING = 4 * BATCH;     // pass-2 staging ring
+constexpr int LONG = 256;           // runs longer than this are copied by the whole wave
+constexpr uint32_t NONE = 0xFFu;
+constexpr int32_t MAX_RUN = 1 << 28;  // length guard (block_max <= 4 MiB in the bulk path)
+
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Diagnostic build only (-DLZ4ADA_IDX_STAMPS): cycles per phase, summed over
+// waves (each stamp drains the wave's memory counters: read shares).
+enum IdxPhase { I_STAGE, I_WALK0, I_ITER, I_CHUNKS, I_ITERS,
+	            D_STAGE, D_WALK1, D_WALK2, D_TLDS, D_THBM, D_NEAR, D_FLUSH, D_GLOBAL,
+	            D_BATCHES, D_GBATCHES, D_ROUNDS, D_TASKS, D_LANES, IDX_NST };
+#ifdef LZ4ADA_IDX_STAMPS
+__device__ unsigned long long g_idx_stamps[IDX_NST];
+#define ISTAMP_DECL uint64_t ist[IDX_NST] = {}; uint64_t ist_t = __builtin_amdgcn_s_memtime()
+#define ISTAMP(ph)                                                           \
+	do {                                                                     \
+		asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");          \
+		const uint64_t _n = __builtin_amdgcn_s_memtime();                    \
+		ist[ph] += _n - ist_t;                                               \
+		ist_t = _n;                                                          \
+	} while (0)
+#define ICOUNT(ph, v) (ist[ph] += uint64_t(v))
+#define ISTAMP_FLUSH()                                                       \
+	do {                                                                     \
+		if (lane_id() == 0)                                                  \
+			for (int _i = 0; _i < IDX_NST; ++_i)                             \
+				atomicAdd(&g_idx_stamps[_i], (unsigned long long)ist[_i]);   \
+	} while (0)
+#else
+#define ISTAMP_DECL
+#define ISTAMP(ph)
+#define ICOUNT(ph, v)
+#define ISTAMP_FLUSH()
+#endif
+
+// ---------------------------------------------------------------- byte access
+// Block-relative byte p comes from LDS when [p, p+8) lies in the staged
+// window [lo, hi), else from global memory (guarded by the frame end).
+struct Src {
+	const uint8_t* lds;  // LDS array; block-relative p at lds[(p + mis) & mask]
+	uint32_t mask;       // LDS array size - 1 (power of two; a 16-byte mirror follows)
+	int32_t mis;
+	int32_t lo, hi;
+	cg8* in;
+	uintptr_t lim;
+};
+
+__device__ __forceinline__ uint32_t fetch4(const Src& S, int32_t p)
+{
+	if (p >= S.lo && p + 8 <= S.hi) {
+		const uint32_t a = uint32_t(p + S.mis) & S.mask;
+		const uint32_t* w = reinterpret_cast<const uint32_t*>(S.lds + (a & ~3u));
+		const uint32_t w0 = w[0], w1 = w[1];  // w[1] may be in the mirror
+		return __builtin_amdgcn_alignbyte(w1, w0, a & 3u);
+	}
+	const uintptr_t g = reinterpret_cast<uintptr_t>(S.in) + uintptr_t(intptr_t(p));
+	uint32_t v = 0;
+#pragma unroll
+	for (int i = 0; i < 4; ++i)
+		if (g + i < S.lim)
+			v |= uint32_t(*reinterpret_cast<cg8*>(g + i)) << (8 * i);
+	return v;
+}
+
+// 16 bytes at block-relative p (literal source): LDS or global.
+__device__ __forceinline__ u32x4 fetch16(const Src& S, int32_t p)
+{
+	if (p >= S.lo && p + 16 <= S.hi)
+		return ld16u(S.lds, uint32_t(p + S.mis) & S.mask, S.mask + 1);
+	const uintptr_t g = reinterpret_cast<uintptr_t>(S.in) + uintptr_t(intptr_t(p));
+	u32x4 v;
+	if (g + 16 <= S.lim) {
+		__builtin_memcpy(&v, reinterpret_cast<cg8*>(g), 16);
+	} else {
+		uint8_t t[16];
+		for (int i = 0; i < 16; ++i)
+			t[i] = (g + i < S.lim) ? *reinterpret_cast<cg8*>(g + i) : 0;
+		__builtin_memcpy(&v, t, 16);
+	}
+	return v;
+}
+
+struct Seq {
+	int32_t lit, L, off, ml, next;  // ml = 0: literal-only last sequence
+};
+
+// One sequence at block-relative p < n (Decompress_Sequence,
+// lz4ada.adb:737-777, with the end-of-block rule of :748-764).  False on
+// any malformed shape; the caller then declines the block.
+__device__ __forceinline__ bool parse_seq(const Src& S, int32_t p, int32_t n, Seq& q)
+{
+	const uint32_t w = fetch4(S, p);
+	const int32_t tk = int32_t(w & 0xffu);
+	int32_t L = tk >> 4, M = tk & 15, x = p + 1;
+	if (L == 15) {
+		uint32_t e, k = 1, ww = w;
+		do {
+			if (x >= n || L > n)
+				return false;
+			if (k > 3) {
+				ww = fetch4(S, x);
+				k = 0;
+			}
+			e = (ww >> (8 * k)) & 0xffu;
+			++k;
+			++x;
+			L += int32_t(e);
+		} while (e == 255u);
+	}
+	q.lit = x;
+	q.L = L;
+	x += L;
+	if (x >= n) {
+		if (x > n || M != 0)
+			return false;
+		q.off = 0;
+		q.ml = 0;
+		q.next = n;
+		return true;
+	}
+	if (x + 1 >= n)
+		return false;
+	uint32_t w2 = fetch4(S, x);
+	q.off = int32_t(w2 & 0xffffu);
+	if (q.off == 0)
+		return false;
+	x += 2;
+	if (M == 15) {
+		uint32_t e, k = 2;
+		do {
+			if (x >= n || M > MAX_RUN)
+				return false;
+			if (k > 3) {
+				w2 = fetch4(S, x);
+				k = 0;
+			}
+			e = (w2 >> (8 * k)) & 0xffu;
+			++k;
+			++x;
+			M += int32_t(e);
+		} while (e == 255u);
+	}
+	q.ml = M + 4;
+	q.next = x;
+	return true;
+}
+
+// 16 bytes from global memory at byte address a, never reading at or past lim.
+__device__ __forceinline__ u32x4 gload16(uintptr_t a, uintptr_t lim)
+{
+	u32x4 v;
+	if (a + 16 <= lim) {
+		__builtin_memcpy(&v, reinterpret_cast<cg8*>(a), 16);
+	} else {
+		uint8_t t[16];
+		for (int i = 0; i < 16; ++i)
+			t[i] = (a + i < lim) ? *reinterpret_cast<cg8*>(a + i) : 0;
+		__builtin_memcpy(&v, t, 16);
+	}
+	return v;
+}
+
+// Exact-length store of n (0..16) bytes to global memory.
+__device__ __forceinline__ void gstore_n(g8* dst, u32x4 v, int32_t n)
+{
+	if (n >= 16) {
+		__builtin_memcpy(dst, &v, 16);
+		return;
+	}
+	uint64_t lo = uint64_t(v.x) | (uint64_t(v.y) << 32);
+	const uint64_t hi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+	if (n & 8) {
+		__builtin_memcpy(dst, &lo, 8);
+		dst += 8;
+		lo = hi;
+	}
+	if (n & 4) {
+		const uint32_t x = uint32_t(lo);
+		__builtin_memcpy(dst, &x, 4);
+		dst += 4;
+		lo >>= 32;
+	}
+	if (n & 2) {
+		const uint16_t x = uint16_t(lo);
+		__builtin_memcpy(dst, &x, 2);
+		dst += 2;
+		lo >>= 16;
+	}
+	if (n & 1)
+		*dst = uint8_t(lo);
+}
+
+// ------------------------------------------------------------------ pass 1
+
+struct alignas(16) IdxLds {
+	uint8_t buf[CHUNK + 16];  // staged chunk; + mirror of its first 16 bytes
+};
+
+// Walk the chain from e (an entry at or after this lane's segment start s)
+// over the sequences starting before seg_end; returns the exit (first
+// chain position >= seg_end, or n).  A malformed sequence sets err and
+// returns seg_end as a guess: from a wrong (speculative) entry that is
+// just a dead chain, and a -1 would poison every lane after it one
+// iteration at a time.  ent collects the index bytes of the segment's 8
+// sub-segments.
+__device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t s, int32_t seg_end,
+                                                int32_t n, uint64_t& ent, bool& err)
+{
+	ent = ~uint64_t(0);
+	err = false;
+	int32_t p = e;
+	while (p < seg_end) {
+		const uint32_t k = uint32_t(p - s) >> 5;
+		const uint64_t cur = (ent >> (8 * k)) & 0xffu;
+		if (cur == NONE)
+			ent ^= (uint64_t(NONE ^ uint32_t((p - s) & 31)) << (8 * k));
+		Seq q;
+		if (!parse_seq(S, p, n, q)) {
+			err = true;
+			return seg_end;
+		}
+		p = q.next;
+	}
+	return p;
+}
+
+// Inclusive prefix maximum over the wave (values >= 0), DPP as wave_incl_scan.
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v)
+{
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));   // row_shr:1
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));   // row_shr:2
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));   // row_shr:4
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));   // row_shr:8
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+	return v;
+}
+
+__global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame, uint64_t frame_len,
+                                               const lz4ada_block_desc* __restrict__ desc,
+                                               uint32_t nblocks, uint8_t* __restrict__ tab_all,
+                                               lz4ada_block_status* __restrict__ status)
+{
+	__shared__ IdxLds X;
+	const uint32_t b = blockIdx.x;
+	if (b >= nblocks)
+		return;
+	const int32_t lane = int32_t(lane_id());
+	const lz4ada_block_desc d = desc[b];
+	if (d.flags & LZ4ADA_BLOCK_STORED) {
+		if (lane == 0)
+			status[b].code = DS_OK;
+		return;
+	}
+	cg8* in = gptr(frame) + d.in_off;
+	const int32_t n = int32_t(d.in_len);
+	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
+	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+	uint64_t* tab = reinterpret_cast<uint64_t*>(tab_all + (((d.in_off >> 8) + b) << 3));
+
+	Src S;
+	S.lds = X.buf;
+	S.mask = CHUNK - 1;
+	S.mis = mis;
+	S.in = in;
+	S.lim = lim;
+
+	// 16 KiB chunk at aligned address a (lanes: 16 x 16 bytes each), the
+	// next one loaded while the current one is walked
+	auto load16k = [&](uintptr_t a, u32x4 (&v)[16]) {
+		if (a + CHUNK <= lim) {
+#pragma unroll
+			for (int r = 0; r < 16; ++r)
+				__builtin_memcpy(&v[r], reinterpret_cast<cg8*>(a + uintptr_t(1024 * r + 16 * lane)), 16);
+		} else {
+#pragma unroll
+			for (int r = 0; r < 16; ++r)
+				v[r] = gload16(a + uintptr_t(1024 * r + 16 * lane), lim);
+		}
+	};
+	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
+	u32x4 pf[16];
+	if (n > 0)
+		load16k(abase, pf);
+
+	ISTAMP_DECL;
+	int32_t E = 0;  // exact chain entry of the current chunk
+	bool bad = false;
+	for (int32_t C = 0; C < n && !bad; C += CHUNK) {
+		// stage block-relative [C - mis, C - mis + CHUNK) (16-byte aligned addresses)
+#pragma unroll
+		for (int r = 0; r < 16; ++r)
+			*reinterpret_cast<u32x4*>(&X.buf[1024 * r + 16 * lane]) = pf[r];
+		if (lane == 0)
+			*reinterpret_cast<u32x4*>(&X.buf[CHUNK]) = pf[0];
+		__syncthreads();
+		if (C + CHUNK < n)
+			load16k(abase + uintptr_t(C + CHUNK), pf);
+		S.lo = C - mis;
+		S.hi = C - mis + CHUNK;
+		ISTAMP(I_STAGE);
+		ICOUNT(I_CHUNKS, 1);
+
+		const int32_t s = C + SEG * lane;
+		const int32_t seg_end = min(s + SEG, n);
+		// Entry of lane i = max exit of lanes < i (lane 0: the exact entry E).
+		// True exits never decrease along the chunk, so the fixed point is
+		// the true chain, and a run of segments a long sequence jumps over
+		// is crossed in one step instead of one iteration per segment.
+		int32_t ein = (lane == 0) ? E : s;
+		uint64_t ent = ~uint64_t(0);
+		bool err = false;
+		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, ent, err) : ein;
+		ISTAMP(I_WALK0);
+		for (int it = 0; it < 64; ++it) {
+			int32_t prev = __shfl_up(wave_incl_max(y), 1);
+			if (lane == 0)
+				prev = E;
+			const bool changed = prev != ein;
+			if (!__any(changed))
+				break;
+			ICOUNT(I_ITERS, 1);
+			if (changed) {
+				ein = prev;
+				if (s < n) {
+					y = walk_segment(S, ein, s, seg_end, n, ent, err);
+				} else {
+					y = ein;
+					err = false;
+				}
+			}
+		}
+		ISTAMP(I_ITER);
+		// converged: every entry is the true chain position
+		if (s < n) {
+			tab[(C >> 8) + lane] = ent;
+			if (err)
+				bad = true;
+		}
+		bad = __any(bad);
+		E = __shfl(wave_incl_max(y), 63);
+		__syncthreads();  // the next chunk overwrites the staging buffer
+	}
+	if (E != n)
+		bad = true;
+	if (lane == 0)
+		status[b].code = bad ? DS_RETRY : DS_OK;
+	ISTAMP_FLUSH();
+}
+
+// ------------------------------------------------------------------ pass 2
+
+// Matches: copy len bytes to ob[dst] from ob[dst - off] (Output_With_History,
+// lz4ada.adb:845-904, for an in-block source).  One lane, exact stores.
+// Sources must be final; for off < len the lane reads back its own first
+// 16 bytes (made visible by a wave-wide wait) or fills an off < 16 pattern.
+__device__ __forceinline__ void lane_match(g8* ob, uintptr_t olim, int32_t dst, int32_t off,
+                                           int32_t len)
+{
+	const uintptr_t base = reinterpret_cast<uintptr_t>(ob);
+	if (off < 16 && off < len) {
+		const u32x4 s = gload16(base + uintptr_t(dst - off), olim);
+		u32x4 pv;
+		int32_t width, stp;
+		make_pattern(uint64_t(s.x) | (uint64_t(s.y) << 32), uint64_t(s.z) | (uint64_t(s.w) << 32),
+		             off, pv, width, stp);
+		for (int32_t k = 0; k < len; k += stp)
+			gstore_n(ob + dst + k, pv, min(width, len - k));
+		return;
+	}
+	int32_t r = 0;
+	for (int32_t k = 0; k < len; k += 16) {
+		const u32x4 v = gload16(base + uintptr_t(dst - off + r), olim);
+		gstore_n(ob + dst + k, v, min(16, len - k));
+		if (k == 0 && off < len)
+			vm_wait();  // bytes [dst, dst+16) are read back by later chunks
+		r += 16;
+		if (r >= off)
+			r -= off;
+	}
+}
+
+// Whole-wave copy of one match (any length).
+__device__ __forceinline__ void wave_match(g8* ob, uintptr_t olim, int32_t dst, int32_t off,
+                                           int32_t len)
+{
+	const int32_t lane = int32_t(lane_id());
+	const uintptr_t base = reinterpret_cast<uintptr_t>(ob);
+	if (off < 16 && off < len) {
+		const u32x4 s = gload16(base + uintptr_t(dst - off), olim);
+		u32x4 pv;
+		int32_t width, stp;
+		make_pattern(uint64_t(s.x) | (uint64_t(s.y) << 32), uint64_t(s.z) | (uint64_t(s.w) << 32),
+		             off, pv, width, stp);
+		for (int32_t c = 0; c < len; c += 64 * stp) {
+			const int32_t k = c + lane * stp;
+			if (k < len)
+				gstore_n(ob + dst + k, pv, min(width, len - k));
+		}
+		return;
+	}
+	// each step copies span <= off bytes, so it reads only bytes already final
+	const int32_t span = off >= 1024 ? 1024 : (off & ~15);
+	for (int32_t c = 0; c < len; c += span) {
+		const int32_t k = c + 16 * lane;
+		if (16 * lane < span && k < len) {
+			const u32x4 v = gload16(base + uintptr_t(dst + k - off), olim);
+			gstore_n(ob + dst + k, v, min(16, len - k));
+		}
+		if (off < len)
+			vm_wait();
+	}
+}
+
+// Whole-wave copy of one literal run from the compressed input.
+__device__ __forceinline__ void wave_literal(g8* ob, int32_t dst, const Src& S, int32_t src,
+                                             int32_t len)
+{
+	const int32_t lane = int32_t(lane_id());
+	for (int32_t c = 0; c < len; c += 1024) {
+		const int32_t k = c + 16 * lane;
+		if (k < len) {
+			const u32x4 v = gload16(reinterpret_cast<uintptr_t>(S.in) + uintptr_t(src + k), S.lim);
+			gstore_n(ob + dst + k, v, min(16, len - k));
+		}
+	}
+}
+
+// Deferred work item of one lane: a long literal run (src >= 0: input
+// position) or a match (src = -offset) that is long or reads this batch.
+struct Item {
+	int32_t dst, len, src;
+};
+
+// Next deferred item of this lane from cursor (p, o, part); part 0 = the
+// sequence's literals are next, 1 = its match.  far_end: output position
+// before which every byte is final (the batch start).
+__device__ __forceinline__ bool next_item(const Src& S, int32_t& p, int32_t& o, int32_t& part,
+                                          int32_t sub_end, int32_t n, int32_t far_end, Item& it)
+{
+	while (p < sub_end) {
+		Seq q;
+		parse_seq(S, p, n, q);  // validated by the first walk of this batch
+		if (part == 0) {
+			part = 1;
+			if (q.L > LONG) {
+				it.dst = o;
+				it.len = q.L;
+				it.src = q.lit;
+				return true;
+			}
+		}
+		const int32_t mdst = o + q.L;
+		p = q.next;
+		o = mdst + q.ml;
+		part = 0;
+		if (q.ml > 0) {
+			const int32_t dep_end = mdst - q.off + min(q.off, q.ml);
+			if (q.ml > LONG || dep_end > far_end) {
+				it.dst = mdst;
+				it.len = q.ml;
+				it.src = -q.off;
+				return true;
+			}
+		}
+	}
+	return false;
+}
+
+// Oversized batches (a lane whose sequences decode to more than the LDS
+// window, e.g. long RLE runs): the batch goes straight to HBM.  Literals
+// and matches reading output older than the batch are copied at once;
+// long runs and matches reading the batch itself follow in output order
+// through a leader loop (the first pending item always runs; any other
+// whose source is already final runs with it), with a wave-wide wait
+// between rounds.  Returns false on a reference before the block start.
+__device__ __forceinline__ bool batch_global(const Src& S, g8* ob, uintptr_t olim, int32_t p0,
+                                          int32_t sub_end, int32_t n, int32_t o_lane,
+                                          int32_t o_batch)
+{
+	const int32_t lane = int32_t(lane_id());
+	int32_t cp = 0, co = 0, cpart = 0;
+	bool has = false, pre = false;
+	{
+		int32_t o = o_lane;
+		for (int32_t p = p0; p < sub_end;) {
+			Seq q;
+			parse_seq(S, p, n, q);
+			if (q.L > LONG) {
+				if (!has) {
+					has = true;
+					cp = p;
+					co = o;
+					cpart = 0;
+				}
+			} else {
+				for (int32_t c = 0; c < q.L; c += 16)
+					gstore_n(ob + o + c, fetch16(S, q.lit + c), min(16, q.L - c));
+			}
+			const int32_t mdst = o + q.L;
+			if (q.ml > 0) {
+				if (q.off > mdst)
+					pre = true;  // reference before the block start (D2)
+				const int32_t dep_end = mdst - q.off + min(q.off, q.ml);
+				if (q.ml > LONG || dep_end > o_batch) {
+					if (!has) {
+						has = true;
+						cp = p;
+						co = o;
+						cpart = 1;
+					}
+				} else if (!pre) {
+					lane_match(ob, olim, mdst, q.off, q.ml);
+				}
+			}
+			o = mdst + q.ml;
+			p = q.next;
+		}
+	}
+	if (__any(pre))
+		return false;
+	Item it = {0, 0, 0};
+	if (has)
+		has = next_item(S, cp, co, cpart, sub_end, n, o_batch, it);
+	if (__any(has)) {
+		vm_wait();  // everything above is final
+		for (;;) {
+			const uint64_t m = __ballot(has);
+			if (m == 0)
+				break;
+			const int32_t leader = __builtin_ctzll(m);
+			const int32_t ldst = __shfl(it.dst, leader);
+			const int32_t llen = __shfl(it.len, leader);
+			const int32_t lsrc = __shfl(it.src, leader);
+			bool ready;
+			if (llen > LONG) {
+				if (lsrc >= 0)
+					wave_literal(ob, ldst, S, lsrc, llen);
+				else
+					wave_match(ob, olim, ldst, -lsrc, llen);
+				ready = (lane == leader);
+			} else {
+				ready = has && it.len <= LONG &&
+				        (it.src >= 0 || it.dst + it.src + min(-it.src, it.len) <= ldst);
+				if (ready) {
+					if (it.src >= 0)
+						for (int32_t c = 0; c < it.len; c += 16)
+							gstore_n(ob + it.dst + c, fetch16(S, it.src + c), min(16, it.len - c));
+					else
+						lane_match(ob, olim, it.dst, -it.src, it.len);
+				}
+			}
+			vm_wait();
+			if (ready)
+				has = next_item(S, cp, co, cpart, sub_end, n, o_batch, it);
+		}
+	}
+	return true;
+}
+
+// ------------------------------------------------------ LDS output window
+// A batch whose output fits in OW bytes is assembled in an LDS ring that
+// also keeps the 2+ KiB of output before it, then flushed to HBM with
+// aligned 16-byte stores (the partial last 16 bytes go with the next batch).
+constexpr int OW = 2032;        // max batch output assembled in LDS (see glo below)
+constexpr int ORING = 4096;     // LDS output ring (batch + history)
+constexpr int OMASK = ORING - 1;
+constexpr int MAXSEQ = 256;     // sequences per batch
+constexpr int RMAX = MAXSEQ / 64;  // rounds of 64 sequences per batch
+constexpr int SLOTS = 12;       // sequence starts in one 32-byte sub-segment (<= 12)
+constexpr int GC = 3;           // 16-byte pieces of an HBM-sourced match loaded ahead
+static_assert(2 * OW + 16 <= ORING, "batch + its HBM threshold must fit the ring");
+
+struct alignas(16) DecLds {
+	uint8_t ring[RING + 16];      // staged input: 4 chunks of 2 KiB (+ mirror)
+	uint8_t oring[ORING];         // output window
+	uint16_t slot[SLOTS][64];     // walk 1: sequence starts of each lane's sub-segment
+	uint16_t cst[MAXSEQ];         // the batch's sequence starts, in order
+	uint32_t pend[(OW + 31) / 32 + 1];  // batch bytes a near match has yet to write
+};
+
+// Exact-length store of n (1..16) bytes at output position x into the ring.
+__device__ __forceinline__ void ostore(DecLds& L, int32_t x, u32x4 v, int32_t n)
+{
+	const uint32_t a = uint32_t(x) & OMASK;
+	if (a + uint32_t(n) <= uint32_t(ORING)) {
+		lds_store_n(&L.oring[a], v, n);
+		return;
+	}
+	const uint64_t lo = uint64_t(v.x) | (uint64_t(v.y) << 32);
+	const uint64_t hi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+	for (int32_t i = 0; i < n; ++i) {
+		const uint64_t w = i < 8 ? lo : hi;
+		L.oring[(a + uint32_t(i)) & OMASK] = uint8_t(w >> (8 * (i & 7)));
+	}
+}
+
+__device__ __forceinline__ u32x4 oload16(const DecLds& L, int32_t x)
+{
+	return ld16u(L.oring, uint32_t(x) & OMASK, ORING);
+}
+
+// Match with a final source entirely inside the ring (Output_With_History,
+// lz4ada.adb:845-904): an off < 16 pattern, else forward 16-byte chunks
+// (a chunk may read bytes the previous chunks of this copy wrote).
+__device__ __forceinline__ void ring_match(DecLds& L, int32_t dst, int32_t off, int32_t len)
+{
+	if (off < 16 && off < len) {
+		const u32x4 s = oload16(L, dst - off);
+		u32x4 pv;
+		int32_t width, stp;
+		make_pattern(uint64_t(s.x) | (uint64_t(s.y) << 32), uint64_t(s.z) | (uint64_t(s.w) << 32),
+		             off, pv, width, stp);
+		for (int32_t k = 0; k < len; k += stp)
+			ostore(L, dst + k, pv, min(width, len - k));
+		return;
+	}
+	for (int32_t k = 0; k < len; k += 16) {
+		const u32x4 v = oload16(L, dst - off + k);
+		wave_lds_fence();
+		ostore(L, dst + k, v, min(16, len - k));
+		wave_lds_fence();
+	}
+}
+
+// pend bits of batch-relative [a, b) (clamped to the batch): all clear?
+__device__ __forceinline__ bool pend_none(const DecLds& L, int32_t a, int32_t b)
+{
+	a = max(a, 0);
+	for (int32_t w = a >> 5; a < b; ++w) {
+		const int32_t lo = a - 32 * w, hi = min(b - 32 * w, 32);
+		const uint32_t m = (hi == 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+		if (L.pend[w] & m)
+			return false;
+		a = 32 * (w + 1);
+	}
+	return true;
+}
+
+// set (or clear) pend bits of batch-relative [a, b)
+__device__ __forceinline__ void pend_mark(DecLds& L, int32_t a, int32_t b, bool set)
+{
+	for (int32_t w = a >> 5; a < b; ++w) {
+		const int32_t lo = a - 32 * w, hi = min(b - 32 * w, 32);
+		const uint32_t m = (hi == 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+		if (set)
+			atomicOr(&L.pend[w], m);
+		else
+			atomicAnd(&L.pend[w], ~m);
+		a = 32 * (w + 1);
+	}
+}
+
+// 2 KiB input chunk c (aligned address abase + c*BATCH), 32 bytes per lane
+__device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_t lim, u32x4& v0,
+                                            u32x4& v1)
+{
+	const uintptr_t g = abase + uintptr_t(c) * BATCH + 16u * lane_id();
+	if (abase + uintptr_t(c + 1) * BATCH <= lim) {
+		__builtin_memcpy(&v0, reinterpret_cast<cg8*>(g), 16);
+		__builtin_memcpy(&v1, reinterpret_cast<cg8*>(g + 1024), 16);
+	} else {
+		v0 = gload16(g, lim);
+		v1 = gload16(g + 1024, lim);
+	}
+}
+
+__global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ frame,
+                                                    uint64_t frame_len,
+                                                    const lz4ada_block_desc* __restrict__ desc,
+                                                    uint32_t nblocks, const uint8_t* __restrict__ tab_all,
+                                                    uint8_t* __restrict__ out,
+                                                    lz4ada_block_status* __restrict__ status)
+{
+	__shared__ DecLds D;
+	const uint32_t b = blockIdx.x;
+	if (b >= nblocks)
+		return;
+	const int32_t lane = int32_t(lane_id());
+	const lz4ada_block_desc d = desc[b];
+	if (status[b].code != DS_OK)
+		return;  // pass 1 declined it
+	cg8* in = gptr(frame) + d.in_off;
+	g8* ob = gptr(out) + d.out_off;
+	const int32_t n = int32_t(d.in_len);
+	const int32_t cap = int32_t(d.out_cap);
+	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
+	const uintptr_t olim = reinterpret_cast<uintptr_t>(ob) + uintptr_t(cap);
+
+	if (d.flags & LZ4ADA_BLOCK_STORED) {
+		int32_t code = DS_OK;
+		if (n > cap) {
+			code = DS_OUT_OVERFLOW;
+		} else {
+			Src S0;
+			S0.in = in;
+			S0.lim = lim;
+			wave_literal(ob, 0, S0, 0, n);
+		}
+		if (lane == 0) {
+			status[b].code = code;
+			status[b].aux = 0;
+			status[b].detail = 0;
+			status[b].err_out_pos = 0;
+			status[b].out_len = code == DS_OK ? uint32_t(n) : 0u;
+		}
+		return;
+	}
+
+	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+	cg8* tab = gptr(tab_all) + (((d.in_off >> 8) + b) << 3);
+	const int32_t nsub = (n + SUB - 1) / SUB;
+	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
+
+	Src S;
+	S.lds = D.ring;
+	S.mask = RING - 1;
+	S.mis = mis;
+	S.in = in;
+	S.lim = lim;
+
+	int32_t hi = 0;  // input chunks staged: [hi - 4, hi) are in the ring
+	u32x4 pf0, pf1;  // chunk hi, loaded ahead
+	load_chunk2(abase, 0, lim, pf0, pf1);
+
+	ISTAMP_DECL;
+	int32_t o_batch = 0;  // output position of the current batch
+	bool bad = false;
+	for (int32_t k0 = 0; k0 < nsub && !bad;) {
+		// stage input so that [k0*SUB, k0*SUB + 4 KiB) is readable
+		const int32_t cf = (k0 * SUB + mis) / BATCH;
+		bool staged = false;
+		if (hi < cf + 3) {
+			staged = true;
+			while (hi < cf + 3) {
+				const uint32_t a = uint32_t(hi * BATCH) & (RING - 1);
+				*reinterpret_cast<u32x4*>(&D.ring[a + 16 * lane]) = pf0;
+				*reinterpret_cast<u32x4*>(&D.ring[a + 1024 + 16 * lane]) = pf1;
+				if (a == 0 && lane == 0)
+					*reinterpret_cast<u32x4*>(&D.ring[RING]) = pf0;
+				++hi;
+				load_chunk2(abase, hi, lim, pf0, pf1);
+			}
+			wave_lds_fence();
+		}
+		S.lo = max(hi - 4, 0) * BATCH - mis;
+		S.hi = hi * BATCH - mis;
+
+		ISTAMP(D_STAGE);
+		ICOUNT(D_BATCHES, 1);
+		const int32_t k = k0 + lane;  // this lane's sub-segment
+		const int32_t sub_s = k * SUB;
+		const int32_t sub_end = min(sub_s + SUB, n);
+		const uint32_t eb = (k < nsub) ? uint32_t(tab[k]) : NONE;
+		const int32_t p0 = (eb == NONE) ? n : sub_s + int32_t(eb);
+
+		// walk 1: output bytes and sequences of this lane
+		int32_t cnt = 0, nseq = 0;
+		bool err = false;
+		for (int32_t p = p0; p < sub_end;) {
+			Seq q;
+			if (!parse_seq(S, p, n, q)) {
+				err = true;
+				break;
+			}
+			cnt += q.L + q.ml;
+			if (nseq < SLOTS)
+				D.slot[nseq][lane] = uint16_t(p - k0 * SUB);
+			++nseq;
+			if (cnt > cap || nseq > SLOTS) {
+				err = true;
+				break;
+			}
+			p = q.next;
+		}
+		if (__any(err)) {
+			bad = true;
+			break;
+		}
+		const int32_t incl = wave_incl_scan(cnt);
+		const int32_t incl_s = wave_incl_scan(nseq);
+		const int32_t o_lane = o_batch + incl - cnt;
+		const bool fit = incl <= OW && incl_s <= MAXSEQ;
+		const int32_t m = __popcll(__ballot(fit));  // lanes [0, m) form an LDS batch
+		ISTAMP(D_WALK1);
+		ICOUNT(D_LANES, m);
+
+		if (m == 0) {
+			// oversized: all 64 sub-segments straight to HBM
+			const int32_t total = __shfl(incl, 63);
+			if (o_batch + total > cap) {
+				bad = true;
+				break;
+			}
+			const int32_t a0 = o_batch & ~15;
+			if (lane == 0 && o_batch > a0)  // the ring's unflushed tail
+				gstore_n(ob + a0, *reinterpret_cast<const u32x4*>(&D.oring[a0 & OMASK]), o_batch - a0);
+			vm_wait();
+			if (!batch_global(S, ob, olim, p0, sub_end, n, o_lane, o_batch)) {
+				bad = true;
+				break;
+			}
+			o_batch += total;
+			vm_wait();
+			ICOUNT(D_GBATCHES, 1);
+			// reload the ring's history from HBM
+			const int32_t u0 = max(o_batch - ORING + 16, 0) >> 4, u1 = (o_batch + 15) >> 4;
+			for (int32_t u = u0 + lane; u < u1; u += 64)
+				*reinterpret_cast<u32x4*>(&D.oring[(u << 4) & OMASK]) =
+				    gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(u << 4), olim);
+			wave_lds_fence();
+			ISTAMP(D_GLOBAL);
+			k0 += 64;
+			continue;
+		}
+
+		const int32_t o_end = o_batch + __shfl(incl, m - 1);
+		if (o_end > cap) {
+			bad = true;
+			break;
+		}
+		// the batch's sequence starts, in output order
+		const int32_t base = k0 * SUB;
+		if (lane < m) {
+			const int32_t e0 = incl_s - nseq;
+			for (int32_t j = 0; j < nseq; ++j)
+				D.cst[e0 + j] = D.slot[j][lane];
+		}
+		D.pend[lane] = 0;
+		wave_lds_fence();
+		const int32_t N = __shfl(incl_s, m - 1);
+		// HBM holds every byte below align_down(o_batch, 16) (earlier
+		// flushes); a match reading below glo reads HBM (its source ends
+		// before o_batch - 16), anything newer is in the ring
+		const int32_t glo = o_batch - OW - 16;
+
+		// P: parse 64 sequences per round, place them by a prefix sum
+		int32_t rL[RMAX], rlit[RMAX], roff[RMAX], rml[RMAX], rdst[RMAX], rbeg[RMAX];
+		bool pre = false, anyg = false;
+		{
+			int32_t o_round = o_batch;
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				rL[r] = rlit[r] = roff[r] = rml[r] = 0;
+				rbeg[r] = o_round;
+				if (64 * r < N) {
+					const int32_t idx = 64 * r + lane;
+					if (idx < N) {
+						Seq q;
+						parse_seq(S, base + int32_t(D.cst[idx]), n, q);
+						rL[r] = q.L;
+						rlit[r] = q.lit;
+						roff[r] = q.off;
+						rml[r] = q.ml;
+					}
+					const int32_t len = rL[r] + rml[r];
+					const int32_t inc = wave_incl_scan(len);
+					rdst[r] = o_round + inc - len;  // literal destination
+					o_round += __shfl(inc, 63);
+					const int32_t mdst = rdst[r] + rL[r];
+					if (rml[r] > 0) {
+						if (roff[r] > mdst)
+							pre = true;  // reference before the block start (D2)
+						if (mdst - roff[r] < glo)
+							anyg = true;
+					}
+				}
+			}
+		}
+		if (__any(pre)) {
+			bad = true;
+			break;
+		}
+		ISTAMP(D_WALK2);
+
+		// HBM-sourced matches: every load in flight before the first use
+		u32x4 vg[RMAX][GC];
+		if (__any(anyg)) {
+			// the previous batch's flush (3 store instructions) and the
+			// input prefetch (2 loads, when this batch staged) may stay in
+			// flight; everything older -- earlier flushes -- is complete
+			if (staged)
+				asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				if (64 * r < N) {
+					const int32_t src = rdst[r] + rL[r] - roff[r];
+					const bool g = rml[r] > 0 && src < glo;
+#pragma unroll
+					for (int c = 0; c < GC; ++c)
+						if (g && 16 * c < rml[r])
+							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
+				}
+			}
+		}
+		ISTAMP(D_TLDS);
+
+		// L: literals (input ring -> output ring)
+#pragma unroll
+		for (int r = 0; r < RMAX; ++r) {
+			if (64 * r < N) {
+				for (int32_t c = 0; c < rL[r]; c += 16)
+					ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), min(16, rL[r] - c));
+			}
+		}
+		wave_lds_fence();
+
+		// M: matches, round by round in output order.  Everything before the
+		// round is final, so a match whose (non-self) source ends there runs
+		// at once; the others wait on the pend bits of the round's pending
+		// near matches.
+#pragma unroll
+		for (int r = 0; r < RMAX; ++r) {
+			if (64 * r < N) {
+				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
+				const int32_t src = mdst - off;
+				const int32_t dep_end = src + min(off, ml);
+				const bool far = ml > 0 && dep_end <= rbeg[r];
+				bool near = ml > 0 && !far;
+				if (far) {
+					if (src < glo) {
+#pragma unroll
+						for (int c = 0; c < GC; ++c)
+							if (16 * c < ml)
+								ostore(D, mdst + 16 * c, vg[r][c], min(16, ml - 16 * c));
+						for (int32_t c = 16 * GC; c < ml; c += 16) {
+							u32x4 v;
+							__builtin_memcpy(&v, ob + src + c, 16);
+							ostore(D, mdst + c, v, min(16, ml - c));
+						}
+					} else {
+						ring_match(D, mdst, off, ml);
+					}
+				}
+				wave_lds_fence();
+				if (__any(near)) {
+					if (near)
+						pend_mark(D, mdst - o_batch, mdst + ml - o_batch, true);
+					wave_lds_fence();
+					while (__any(near)) {
+						ICOUNT(D_ROUNDS, 1);
+						const bool ready = near && pend_none(D, src - o_batch, dep_end - o_batch);
+						wave_lds_fence();
+						if (ready)
+							ring_match(D, mdst, off, ml);
+						wave_lds_fence();
+						if (ready) {
+							pend_mark(D, mdst - o_batch, mdst + ml - o_batch, false);
+							near = false;
+						}
+						wave_lds_fence();
+					}
+				}
+			}
+		}
+		ISTAMP(D_NEAR);
+
+		// flush whole 16-byte units of [o_batch, o_end) (the first may start
+		// before o_batch: those bytes are in the ring too); always three
+		// store instructions, so the wait above can count them
+		{
+			const int32_t u0 = o_batch >> 4, u1 = o_end >> 4;
+#pragma unroll
+			for (int i = 0; i < 3; ++i) {
+				const int32_t u = u0 + lane + 64 * i;
+				if (u < u1)
+					*reinterpret_cast<GLOBAL u32x4*>(ob + (u << 4)) =
+					    *reinterpret_cast<const u32x4*>(&D.oring[(u << 4) & OMASK]);
+			}
+		}
+		o_batch = o_end;
+		k0 += m;
+		ISTAMP(D_FLUSH);
+	}
+	if (!bad && lane == 0 && (o_batch & 15))  // last partial unit
+		gstore_n(ob + (o_batch & ~15), *reinterpret_cast<const u32x4*>(&D.oring[(o_batch & ~15) & OMASK]),
+		         o_batch & 15);
+	if (lane == 0) {
+		if (bad) {
+			status[b].code = DS_RETRY;
+		} else {
+			status[b].code = DS_OK;
+			status[b].aux = 0;
+			status[b].detail = 0;
+			status[b].err_out_pos = 0;
+			status[b].out_len = uint32_t(o_batch);
+		}
+	}
+	ISTAMP_FLUSH();
+}
+
+}  // namespace idx
+
+#ifdef LZ4ADA_IDX_STAMPS
+extern "C" int lz4ada_idx_stamps(unsigned long long* out, int reset)
+{
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(idx::g_idx_stamps),
+	                        sizeof(unsigned long long) * idx::IDX_NST) != hipSuccess)
+		return -1;
+	if (reset) {
+		unsigned long long z[idx::IDX_NST] = {};
+		if (hipMemcpyToSymbol(HIP_SYMBOL(idx::g_idx_stamps), z, sizeof z) != hipSuccess)
+			return -1;
+	}
+	return idx::IDX_NST;
+}
+#endif
+
+hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
+                             const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
+                             lz4ada_block_status* d_status, hipStream_t stream)
+{
+	if (nblocks == 0)
+		return hipSuccess;
+	// index table: 8 bytes per 256-byte segment, per block at ((in_off >> 8) + b) * 8
+	const size_t tab_len = ((size_t(frame_len) >> 8) + size_t(nblocks) + 2) * 8;
+	void* tab = nullptr;
+	hipError_t err = hipMallocAsync(&tab, tab_len, stream);
+	if (err != hipSuccess)
+		return err;
+	hipLaunchKernelGGL(idx::k_index, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len, d_desc,
+	                   nblocks, static_cast<uint8_t*>(tab), d_status);
+	hipLaunchKernelGGL(idx::k_decode_idx, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
+	                   d_desc, nblocks, static_cast<const uint8_t*>(tab), d_out, d_status);
+	err = hipGetLastError();
+	const hipError_t e2 = hipFreeAsync(tab, stream);
+	return err != hipSuccess ? err : e2;
+}
+
+}  // namespace lz4ada

@@ -52,7 +52,7 @@ struct SerialState {
 // All launch on `stream` and never synchronise.
 
 // Bulk independent-block decoders (LZ4ADA_DECODE_* in lz4ada_hip.h).
-enum DecVariant : int { DEC_PC = 0, DEC_WAVE = 1, DEC_WG = 2 };
+enum DecVariant : int { DEC_PC = 0, DEC_WAVE = 1, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4 };
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
@@ -71,6 +71,12 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
 hipError_t launch_decode_wg(const uint8_t* d_frame, uint64_t frame_len,
                             const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
                             lz4ada_block_status* d_status, hipStream_t stream);
+
+// Index-driven decoder alone (lz4ada_idx.hip): k_index + k_decode_idx;
+// declined blocks keep status DS_RETRY and are not decoded.
+hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
+                             const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
+                             lz4ada_block_status* d_status, hipStream_t stream);
 
 // Per-block XXH32 of the compressed payloads (block checksums).
 hipError_t launch_block_checksums(const uint8_t* d_frame,

@@ -2012,6 +2012,15 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 		                   d_desc, nblocks, d_out, d_status, 0);
 		return hipGetLastError();
 	}
+	if (variant == DEC_IDX || variant == DEC_IDX_ALONE) {
+		const hipError_t err = launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out,
+		                                         d_status, stream);
+		if (err != hipSuccess || variant == DEC_IDX_ALONE)
+			return err;
+		hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
+		                   d_desc, nblocks, d_out, d_status, 1);
+		return hipGetLastError();
+	}
 	if (variant == DEC_WG) {
 		const hipError_t err = launch_decode_wg(d_frame, frame_len, d_desc, nblocks, d_out,
 		                                        d_status, stream);
@@ -2035,6 +2044,8 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
 		const char* e = getenv("LZ4ADA_DECODER");
 		if (e && e[0] == 'w' && e[1] == 'g')
 			return int(DEC_WG);
+		if (e && e[0] == 'i')
+			return int(DEC_IDX);
 		if (e && e[0] == 'w')
 			return int(DEC_WAVE);
 		return int(DEC_PC);

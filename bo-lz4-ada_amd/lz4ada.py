@@ -385,7 +385,7 @@ def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=
                                      stream), _thread_error())
 
 
-DECODE_PC, DECODE_WAVE, DECODE_WG = 0, 1, 2
+DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE = 0, 1, 2, 3, 4
 
 
 def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,

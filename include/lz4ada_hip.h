@@ -220,6 +220,11 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
 #define LZ4ADA_DECODE_PC 0
 #define LZ4ADA_DECODE_WAVE 1
 #define LZ4ADA_DECODE_WG 2
+/* Index-driven two-pass decoder (k_index + k_decode_idx, lz4ada_idx.hip),
+ * then the two-wave decoder for the blocks it declines; _ALONE skips that
+ * second step (declined blocks keep status code 10). */
+#define LZ4ADA_DECODE_IDX 3
+#define LZ4ADA_DECODE_IDX_ALONE 4
 int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                                  lz4ada_block_status *d_status, int variant, void *stream);

@@ -253,7 +253,7 @@ def test_device_resident_blocks():
 
 # ------------------------------------------- bench-sized blocks (regression)
 
-@pytest.mark.parametrize("variant", ["pc", "wave", "wg"])
+@pytest.mark.parametrize("variant", ["pc", "wave", "wg", "idx"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
 def test_bench_blocks_exact(kind, variant):
     """The bench's own unique 4 MiB blocks (seed 0x4C5A3441 + i) decode
@@ -273,7 +273,8 @@ def test_bench_blocks_exact(kind, variant):
     d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
     sh = torch.cuda.current_stream().cuda_stream
     lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), nb, d_st.data_ptr(), sh)
-    v = {"pc": lz4ada.DECODE_PC, "wave": lz4ada.DECODE_WAVE, "wg": lz4ada.DECODE_WG}[variant]
+    v = {"pc": lz4ada.DECODE_PC, "wave": lz4ada.DECODE_WAVE, "wg": lz4ada.DECODE_WG,
+         "idx": lz4ada.DECODE_IDX}[variant]
     lz4ada.launch_decode_variant(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
                                  d_out.data_ptr(), d_st.data_ptr(), v, sh)
     torch.cuda.synchronize()
@@ -372,3 +373,82 @@ def test_wg_decoder_alone_on_vectors(name, digests):
         pieces.append(out[i * info.block_max:i * info.block_max + st[i].out_len])
     if all_ok and info.independent:
         assert hashlib.sha256(b"".join(pieces)).hexdigest() == digests[name]["sha256"]
+
+
+def _run_variant_alone(frame, variant):
+    """Decode a frame's blocks with one decoder variant and no retry pass;
+    returns (descs, statuses, output bytes)."""
+    import torch
+    info, descs = lz4ada.frame_index(frame)
+    nb = info.nblocks
+    bmax = info.block_max
+    dev = torch.device("cuda:0")
+    d_frame = torch.frombuffer(bytearray(frame), dtype=torch.uint8).to(dev)
+    d_desc = torch.frombuffer(bytearray(bytes(descs)[:nb * 32]), dtype=torch.uint8).to(dev)
+    d_out = torch.zeros(nb * bmax, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
+    lz4ada.launch_decode_variant(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
+                                 d_out.data_ptr(), d_st.data_ptr(), variant,
+                                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    st = (lz4ada.BlockStatus * nb).from_buffer_copy(d_st.cpu().numpy().tobytes())
+    return descs, st, d_out.cpu().numpy().tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "rle"])
+@pytest.mark.parametrize("bmax", [64 << 10, 256 << 10, 4 << 20])
+def test_idx_decoder_alone(kind, bmax):
+    """k_index + k_decode_idx on their own: exact output for every block they
+    accept, and they accept every well-formed independent block."""
+    blocks = [lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 0x4C5A3441 + i, bmax) for i in range(6)]
+    blocks.append(lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 77, 1000))  # short last block
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, indep=True)
+    descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX_ALONE)
+    bad = []
+    for i, (c, r) in enumerate(blocks):
+        got = out[i * bmax:i * bmax + len(r)]
+        if st[i].code or st[i].out_len != len(r) or got != r:
+            j = next((k for k in range(min(len(r), len(got))) if got[k] != r[k]), -1)
+            bad.append((i, st[i].code, st[i].out_len, len(r), j))
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_idx_decoder_stored_and_small():
+    """Stored blocks, tiny blocks and an empty block through the idx decoder."""
+    blocks = []
+    for i in range(9):
+        raw_len = [65536, 1, 0, 13, 100, 65536, 4000, 31, 33][i]
+        if i in (5, 6):
+            raw = random.Random(500 + i).randbytes(raw_len)
+            blocks.append((raw, raw, True))
+        else:
+            comp, raw = lz4ada.gen_block(i % 4, 500 + i, raw_len)
+            blocks.append((comp, raw, False))
+    frame, raw = lz4frame.build_frame(blocks, 64 << 10, indep=True, block_cksum=True)
+    info, descs = lz4ada.frame_index(frame)
+    descs_, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX)
+    got = b"".join(out[i * info.block_max:i * info.block_max + st[i].out_len]
+                   for i in range(info.nblocks))
+    assert all(s.code == 0 for s in st[:info.nblocks])
+    assert got == raw
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
+def test_idx_decoder_on_vectors(name, digests):
+    """Reference vectors' blocks through the idx decoder (+ retry): every block
+    byte-exact; linked blocks that reference earlier blocks are declined
+    (DS_RETRY) by the idx pass and redone exactly."""
+    frame = read_vector(name, "lz4")
+    info, _ = lz4ada.frame_index(frame)
+    descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX_ALONE)
+    for i in range(info.nblocks):
+        assert st[i].code in (0, lz4ada.DS_RETRY), (i, st[i].code)
+    descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX)
+    if info.independent or all(s.code == 0 for s in st[:info.nblocks]):
+        pieces = [out[i * info.block_max:i * info.block_max + st[i].out_len]
+                  for i in range(info.nblocks)]
+        if all(s.code == 0 for s in st[:info.nblocks]):
+            assert hashlib.sha256(b"".join(pieces)).hexdigest() == digests[name]["sha256"]
