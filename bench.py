@@ -45,7 +45,8 @@ import lz4frame  # noqa: E402
 METRIC = "decompressed MiB/s + achieved HBM GB/s vs roofline, 4MiB-block frame @1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # decode kernel each LZ4ADA_DECODER setting launches (lz4ada_kernels.hip launch_decode_blocks)
-DECODE_KERNEL = {"pc": "k_decode_pc", "wave": "k_decode_blocks", "wg": "k_decode_wg"}
+DECODE_KERNEL = {"idx": "k_index+k_decode_idx", "pc": "k_decode_pc", "wave": "k_decode_blocks",
+                 "wg": "k_decode_wg"}
 SEED0 = 0x4C5A3441
 MiB = 1 << 20
 
@@ -238,7 +239,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     total_raw = raw_bytes * world * args.steps
     value = total_raw / elapsed / MiB
-    dec_kernel = DECODE_KERNEL[os.environ.get("LZ4ADA_DECODER", "pc")]
+    dec_kernel = DECODE_KERNEL[os.environ.get("LZ4ADA_DECODER", "idx")]
     alg_bytes = comp_bytes + raw_bytes  # compressed read once + output written once
     achieved = alg_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None

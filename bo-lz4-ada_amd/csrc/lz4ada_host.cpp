@@ -766,8 +766,8 @@ struct lz4ada_decompressor {
 		if (bcl)
 			HIP_OK(launch_block_checksums(ahead.d_in.p, ahead.d_desc.p, uint32_t(nb), ahead.d_st.p,
 			                              stream));
-		HIP_OK(launch_decode_variant(ahead.d_in.p, uint64_t(pos), ahead.d_desc.p, uint32_t(nb),
-		                             ahead.d_out.p, ahead.d_st.p, DEC_PC, stream));
+		HIP_OK(launch_decode_blocks(ahead.d_in.p, uint64_t(pos), ahead.d_desc.p, uint32_t(nb),
+		                            ahead.d_out.p, ahead.d_st.p, stream));
 		HIP_OK(hipMemcpyAsync(ahead.st.data(), ahead.d_st.p, nb * sizeof(lz4ada_block_status),
 		                      hipMemcpyDeviceToHost, stream));
 		HIP_OK(hipStreamSynchronize(stream));

@@ -54,7 +54,7 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::
 // Diagnostic build only (-DLZ4ADA_IDX_STAMPS): cycles per phase, summed over
 // waves (each stamp drains the wave's memory counters: read shares).
 enum IdxPhase { I_STAGE, I_WALK0, I_ITER, I_CHUNKS, I_ITERS,
-	            D_STAGE, D_WALK1, D_WALK2, D_TLDS, D_THBM, D_NEAR, D_FLUSH, D_GLOBAL,
+	            D_STAGE, D_WALK1, D_WALK2, D_TLDS, D_LIT, D_MFAR, D_NEAR, D_FLUSH, D_GLOBAL,
 	            D_BATCHES, D_GBATCHES, D_ROUNDS, D_TASKS, D_LANES, IDX_NST };
 #ifdef LZ4ADA_IDX_STAMPS
 __device__ unsigned long long g_idx_stamps[IDX_NST];
@@ -192,6 +192,36 @@ __device__ __forceinline__ bool parse_seq(const Src& S, int32_t p, int32_t n, Se
 	return true;
 }
 
+// parse_seq for the common shape, without branches: both length
+// extensions at most one byte, every byte read in the LDS window, the
+// sequence well before the block end.  Anything else (and malformed data)
+// takes parse_seq; the result is the same.
+__device__ __forceinline__ bool parse_fast(const Src& S, int32_t p, int32_t n, Seq& q)
+{
+	const uint32_t a = uint32_t(p + S.mis) & S.mask;
+	const uint32_t* wa = reinterpret_cast<const uint32_t*>(S.lds + (a & ~3u));
+	const uint32_t w = __builtin_amdgcn_alignbyte(wa[1], wa[0], a & 3u);
+	const uint32_t tk = w & 0xffu, e1 = (w >> 8) & 0xffu;
+	const bool x1 = tk >= 0xf0u, x2 = (tk & 15u) == 15u;
+	const int32_t L = int32_t(tk >> 4) + (x1 ? int32_t(e1) : 0);
+	const int32_t lit = p + 1 + (x1 ? 1 : 0);
+	const int32_t x = lit + L;
+	const uint32_t b = uint32_t(x + S.mis) & S.mask;
+	const uint32_t* wb = reinterpret_cast<const uint32_t*>(S.lds + (b & ~3u));
+	const uint32_t w2 = __builtin_amdgcn_alignbyte(wb[1], wb[0], b & 3u);
+	const uint32_t e2 = (w2 >> 16) & 0xffu;
+	q.lit = lit;
+	q.L = L;
+	q.off = int32_t(w2 & 0xffffu);
+	q.ml = int32_t(tk & 15u) + 4 + (x2 ? int32_t(e2) : 0);
+	q.next = x + 2 + (x2 ? 1 : 0);
+	const bool ok = p >= S.lo && x + 8 <= S.hi && x + 8 <= n && !(x1 && e1 == 255u) &&
+	                !(x2 && e2 == 255u) && q.off != 0;
+	if (__builtin_expect(ok, 1))
+		return true;
+	return parse_seq(S, p, n, q);
+}
+
 // 16 bytes from global memory at byte address a, never reading at or past lim.
 __device__ __forceinline__ u32x4 gload16(uintptr_t a, uintptr_t lim)
 {
@@ -262,7 +292,7 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 		if (cur == NONE)
 			ent ^= (uint64_t(NONE ^ uint32_t((p - s) & 31)) << (8 * k));
 		Seq q;
-		if (!parse_seq(S, p, n, q)) {
+		if (!parse_fast(S, p, n, q)) {
 			err = true;
 			return seg_end;
 		}
@@ -386,6 +416,19 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 		}
 		bad = __any(bad);
 		E = __shfl(wave_incl_max(y), 63);
+		if (C == 0 && n >= 4 * CHUNK) {
+			// Sparse chains (over 64 input bytes per sequence: long literal
+			// runs) defeat the speculative walks -- every segment's guess
+			// misses and the entries crawl one lane per iteration -- and are
+			// the one-wave scalar parse's best case: decline the block (large
+			// blocks only: a short one costs a few chunks either way).
+			int32_t used = 0;
+#pragma unroll
+			for (int k = 0; k < NSUB; ++k)
+				used += ((ent >> (8 * k)) & 0xffu) != NONE ? 1 : 0;
+			if (__shfl(wave_incl_scan(used), 63) < CHUNK / SUB / 4)
+				bad = true;
+		}
 		__syncthreads();  // the next chunk overwrites the staging buffer
 	}
 	if (E != n)
@@ -623,7 +666,6 @@ struct alignas(16) DecLds {
 	uint8_t oring[ORING];         // output window
 	uint16_t slot[SLOTS][64];     // walk 1: sequence starts of each lane's sub-segment
 	uint16_t cst[MAXSEQ];         // the batch's sequence starts, in order
-	uint32_t pend[(OW + 31) / 32 + 1];  // batch bytes a near match has yet to write
 };
 
 // Exact-length store of n (1..16) bytes at output position x into the ring.
@@ -670,32 +712,16 @@ __device__ __forceinline__ void ring_match(DecLds& L, int32_t dst, int32_t off, 
 	}
 }
 
-// pend bits of batch-relative [a, b) (clamped to the batch): all clear?
-__device__ __forceinline__ bool pend_none(const DecLds& L, int32_t a, int32_t b)
+// Owner of piece t when lane i holds pieces [inc_i - cnt_i, inc_i) (inc: the
+// wave's inclusive prefix sum of piece counts): the first lane with inc > t.
+__device__ __forceinline__ int32_t piece_owner(int32_t inc, int32_t t)
 {
-	a = max(a, 0);
-	for (int32_t w = a >> 5; a < b; ++w) {
-		const int32_t lo = a - 32 * w, hi = min(b - 32 * w, 32);
-		const uint32_t m = (hi == 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-		if (L.pend[w] & m)
-			return false;
-		a = 32 * (w + 1);
-	}
-	return true;
-}
-
-// set (or clear) pend bits of batch-relative [a, b)
-__device__ __forceinline__ void pend_mark(DecLds& L, int32_t a, int32_t b, bool set)
-{
-	for (int32_t w = a >> 5; a < b; ++w) {
-		const int32_t lo = a - 32 * w, hi = min(b - 32 * w, 32);
-		const uint32_t m = (hi == 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-		if (set)
-			atomicOr(&L.pend[w], m);
-		else
-			atomicAnd(&L.pend[w], ~m);
-		a = 32 * (w + 1);
-	}
+	int32_t lo = 0;
+#pragma unroll
+	for (int st = 32; st >= 1; st >>= 1)
+		if (__shfl(inc, lo + st - 1) <= t)
+			lo += st;
+	return lo;
 }
 
 // 2 KiB input chunk c (aligned address abase + c*BATCH), 32 bytes per lane
@@ -806,7 +832,7 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 		bool err = false;
 		for (int32_t p = p0; p < sub_end;) {
 			Seq q;
-			if (!parse_seq(S, p, n, q)) {
+			if (!parse_fast(S, p, n, q)) {
 				err = true;
 				break;
 			}
@@ -873,7 +899,6 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 			for (int32_t j = 0; j < nseq; ++j)
 				D.cst[e0 + j] = D.slot[j][lane];
 		}
-		D.pend[lane] = 0;
 		wave_lds_fence();
 		const int32_t N = __shfl(incl_s, m - 1);
 		// HBM holds every byte below align_down(o_batch, 16) (earlier
@@ -894,7 +919,7 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 					const int32_t idx = 64 * r + lane;
 					if (idx < N) {
 						Seq q;
-						parse_seq(S, base + int32_t(D.cst[idx]), n, q);
+						parse_fast(S, base + int32_t(D.cst[idx]), n, q);
 						rL[r] = q.L;
 						rlit[r] = q.lit;
 						roff[r] = q.off;
@@ -944,57 +969,120 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 		}
 		ISTAMP(D_TLDS);
 
-		// L: literals (input ring -> output ring)
+		// L: literals (input ring -> output ring).  Short runs lane by lane;
+		// a round with a run over 32 bytes deals its 16-byte pieces over the
+		// whole wave instead.
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
 			if (64 * r < N) {
-				for (int32_t c = 0; c < rL[r]; c += 16)
-					ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), min(16, rL[r] - c));
+#ifdef LZ4ADA_IDX_EXP_NOLIT
+				if (1) continue;
+#endif
+				const int32_t nc = (rL[r] + 15) >> 4;
+				if (__any(nc > 2)) {
+					const int32_t inc = wave_incl_scan(nc);
+					const int32_t tot = __shfl(inc, 63);
+					for (int32_t t0 = 0; t0 < tot; t0 += 64) {
+						const int32_t t = t0 + lane;
+						const int32_t lo = piece_owner(inc, t);
+						const int32_t k = t - (__shfl(inc, lo) - __shfl(nc, lo));
+						const int32_t L = __shfl(rL[r], lo);
+						const int32_t lit = __shfl(rlit[r], lo);
+						const int32_t dst = __shfl(rdst[r], lo);
+						if (t < tot)
+							ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, L - 16 * k));
+					}
+				} else {
+					for (int32_t c = 0; c < rL[r]; c += 16)
+						ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), min(16, rL[r] - c));
+				}
 			}
 		}
 		wave_lds_fence();
+		ISTAMP(D_LIT);
 
 		// M: matches, round by round in output order.  Everything before the
-		// round is final, so a match whose (non-self) source ends there runs
-		// at once; the others wait on the pend bits of the round's pending
-		// near matches.
+		// round is final, so a match whose (non-self) source ends there (or
+		// lies in its own literals) runs at once; a near match -- one reading
+		// this round's match output -- runs once every lane it reads from is
+		// done.
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
 			if (64 * r < N) {
 				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
 				const int32_t src = mdst - off;
 				const int32_t dep_end = src + min(off, ml);
-				const bool far = ml > 0 && dep_end <= rbeg[r];
+				// runs now: a source before the round, or inside this
+				// sequence's own literals (off <= L)
+				const bool far = ml > 0 && (dep_end <= rbeg[r] || off <= rL[r]);
 				bool near = ml > 0 && !far;
+				const bool hbm = far && src < glo;
 				if (far) {
-					if (src < glo) {
+					if (hbm) {
+#ifndef LZ4ADA_IDX_EXP_NOHBMST
 #pragma unroll
 						for (int c = 0; c < GC; ++c)
 							if (16 * c < ml)
 								ostore(D, mdst + 16 * c, vg[r][c], min(16, ml - 16 * c));
-						for (int32_t c = 16 * GC; c < ml; c += 16) {
-							u32x4 v;
-							__builtin_memcpy(&v, ob + src + c, 16);
-							ostore(D, mdst + c, v, min(16, ml - c));
-						}
+#endif
 					} else {
+#ifndef LZ4ADA_IDX_EXP_NORING
 						ring_match(D, mdst, off, ml);
+#endif
+					}
+				}
+				// pieces of HBM-sourced matches beyond the first GC: dealt over
+				// the wave, so 64 loads are in flight at once
+				{
+					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;
+					if (__any(nc > 0)) {
+						const int32_t inc = wave_incl_scan(nc);
+						const int32_t tot = __shfl(inc, 63);
+						for (int32_t t0 = 0; t0 < tot; t0 += 64) {
+							const int32_t t = t0 + lane;
+							const int32_t lo = piece_owner(inc, t);
+							const int32_t k = GC + t - (__shfl(inc, lo) - __shfl(nc, lo));
+							const int32_t osrc = __shfl(src, lo), odst = __shfl(mdst, lo);
+							const int32_t oml = __shfl(ml, lo);
+							if (t < tot) {
+								u32x4 v;
+								__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
+								ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
+							}
+						}
 					}
 				}
 				wave_lds_fence();
+				ISTAMP(D_MFAR);
+#ifdef LZ4ADA_IDX_EXP_NONEAR
+				near = false;
+#endif
 				if (__any(near)) {
-					if (near)
-						pend_mark(D, mdst - o_batch, mdst + ml - o_batch, true);
-					wave_lds_fence();
-					while (__any(near)) {
+					// lanes whose match output this near match reads: those
+					// with mend > src and mdst < dep_end (both monotone along
+					// the round, so two binary searches)
+					const int32_t mend = mdst + ml;
+					int32_t j1 = 0, c2 = 0;
+#pragma unroll
+					for (int st = 32; st >= 1; st >>= 1) {
+						if (__shfl(mend, j1 + st - 1) <= src)
+							j1 += st;
+						if (__shfl(mdst, c2 + st - 1) < dep_end)
+							c2 += st;
+					}
+					const int32_t j2 = min(c2 - 1, lane - 1);
+					uint64_t dep = 0;
+					if (near && j1 <= j2)
+						dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) &
+						      ~((uint64_t(1) << j1) - 1);
+					for (;;) {
+						const uint64_t pending = __ballot(near);
+						if (pending == 0)
+							break;
 						ICOUNT(D_ROUNDS, 1);
-						const bool ready = near && pend_none(D, src - o_batch, dep_end - o_batch);
-						wave_lds_fence();
-						if (ready)
-							ring_match(D, mdst, off, ml);
-						wave_lds_fence();
+						const bool ready = near && (dep & pending) == 0;
 						if (ready) {
-							pend_mark(D, mdst - o_batch, mdst + ml - o_batch, false);
+							ring_match(D, mdst, off, ml);
 							near = false;
 						}
 						wave_lds_fence();

@@ -2037,18 +2037,18 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
                                 uint8_t* d_out, lz4ada_block_status* d_status,
                                 hipStream_t stream)
 {
-	// Default: the two-wave producer/consumer decoder.  LZ4ADA_DECODER=wave
-	// selects the one-wave decoder, LZ4ADA_DECODER=wg the experimental
-	// workgroup decoder (one-wave decoder for the blocks it declines).
+	// Default: the index-driven decoder (lz4ada_idx.hip), the two-wave
+	// decoder for the blocks it declines.  LZ4ADA_DECODER=pc / wave / wg
+	// select the two-wave, one-wave or experimental workgroup decoder.
 	static const int variant = [] {
 		const char* e = getenv("LZ4ADA_DECODER");
 		if (e && e[0] == 'w' && e[1] == 'g')
 			return int(DEC_WG);
-		if (e && e[0] == 'i')
-			return int(DEC_IDX);
+		if (e && e[0] == 'p')
+			return int(DEC_PC);
 		if (e && e[0] == 'w')
 			return int(DEC_WAVE);
-		return int(DEC_PC);
+		return int(DEC_IDX);
 	}();
 	return launch_decode_variant(d_frame, frame_len, d_desc, nblocks, d_out, d_status, variant,
 	                             stream);

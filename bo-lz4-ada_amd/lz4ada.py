@@ -390,7 +390,8 @@ DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE = 0, 1, 2, 3, 4
 
 def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,
                           stream=0):
-    """One of the bulk decoders (DECODE_PC default, DECODE_WAVE, DECODE_WG)."""
+    """One of the bulk decoders: DECODE_IDX (default: index-driven + two-wave
+    retry), DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX_ALONE."""
     _check(_lib.lz4ada_launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out,
                                              d_status, variant, stream), _thread_error())
 

