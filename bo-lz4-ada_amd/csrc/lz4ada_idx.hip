@@ -652,13 +652,14 @@ __device__ __forceinline__ bool batch_global(const Src& S, g8* ob, uintptr_t oli
 // A batch whose output fits in OW bytes is assembled in an LDS ring that
 // also keeps the 2+ KiB of output before it, then flushed to HBM with
 // aligned 16-byte stores (the partial last 16 bytes go with the next batch).
-constexpr int OW = 2032;        // max batch output assembled in LDS (see glo below)
-constexpr int ORING = 4096;     // LDS output ring (batch + history)
+constexpr int OW = 4080;        // max batch output assembled in LDS (see glo below)
+constexpr int ORING = 8192;     // LDS output ring (batch + history)
 constexpr int OMASK = ORING - 1;
 constexpr int MAXSEQ = 256;     // sequences per batch
 constexpr int RMAX = MAXSEQ / 64;  // rounds of 64 sequences per batch
 constexpr int SLOTS = 12;       // sequence starts in one 32-byte sub-segment (<= 12)
 constexpr int GC = 3;           // 16-byte pieces of an HBM-sourced match loaded ahead
+constexpr int FLUSH_ST = (OW + 15) / 16 / 64 + 1;  // store instructions per flush (fixed)
 static_assert(2 * OW + 16 <= ORING, "batch + its HBM threshold must fit the ring");
 
 struct alignas(16) DecLds {
@@ -948,13 +949,14 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 		// HBM-sourced matches: every load in flight before the first use
 		u32x4 vg[RMAX][GC];
 		if (__any(anyg)) {
-			// the previous batch's flush (3 store instructions) and the
-			// input prefetch (2 loads, when this batch staged) may stay in
-			// flight; everything older -- earlier flushes -- is complete
+			// the previous batch's flush (FLUSH_ST store instructions) and
+			// the input prefetch (2 loads, when this batch staged) may stay
+			// in flight; everything older -- earlier flushes -- is complete
+			static_assert(FLUSH_ST == 4, "update the counted waits");
 			if (staged)
-				asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+				asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
 			else
-				asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+				asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
 				if (64 * r < N) {
@@ -1093,12 +1095,12 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 		ISTAMP(D_NEAR);
 
 		// flush whole 16-byte units of [o_batch, o_end) (the first may start
-		// before o_batch: those bytes are in the ring too); always three
+		// before o_batch: those bytes are in the ring too); always FLUSH_ST
 		// store instructions, so the wait above can count them
 		{
 			const int32_t u0 = o_batch >> 4, u1 = o_end >> 4;
 #pragma unroll
-			for (int i = 0; i < 3; ++i) {
+			for (int i = 0; i < FLUSH_ST; ++i) {
 				const int32_t u = u0 + lane + 64 * i;
 				if (u < u1)
 					*reinterpret_cast<GLOBAL u32x4*>(ob + (u << 4)) =
