@@ -23,8 +23,9 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_decode_pc", "k_decode_wg", "k_decode_blocks", "k_block_checksums", "k_output_checksums", "k_serial_block",
-           "k_xxh32_update", "k_compact")
+KERNELS = ("k_decode_idx", "k_index", "k_decode_pc", "k_decode_wg", "k_decode_blocks",
+           "k_block_checksums", "k_output_checksums", "k_serial_block", "k_xxh32_update",
+           "k_compact")
 
 
 def short(name):
@@ -86,8 +87,18 @@ def main():
     with open(os.path.join(prof, f"{args.tag}_pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1)
 
-    dname = next((k for k in ("k_decode_pc", "k_decode_blocks") if k in out["kernels"]), None)
-    dec = out["kernels"].get(dname, {})
+    ks = out["kernels"]
+    if "k_decode_idx" in ks and "k_index" in ks:
+        # the default decode path is two kernels: report their sum per launch
+        a, b = ks["k_index"], ks["k_decode_idx"]
+        dname = "k_index+k_decode_idx"
+        dec = {}
+        for f in ("hbm_bytes_per_launch", "fetch_bytes_x2", "write_bytes", "avg_ns"):
+            if f in a and f in b:
+                dec[f] = a[f] + b[f]
+    else:
+        dname = next((k for k in ("k_decode_pc", "k_decode_blocks") if k in ks), None)
+        dec = ks.get(dname, {})
     if "hbm_bytes_per_launch" in dec:
         pj = {"config": {"kind": args.kind, "blocks": args.blocks, "block_max": args.block_max},
               "kernel": dname,
