@@ -109,11 +109,34 @@ __device__ __forceinline__ uint32_t fetch4(const Src& S, int32_t p)
 	return v;
 }
 
+// 16 bytes at byte a of a power-of-two LDS ring (mask = size - 1): three
+// 8-byte-aligned ds_read_b64 (each wrapped on its own), a one-bit dword
+// select and four v_alignbyte -- ld16u's select network costs ~4x the VALU.
+__device__ __forceinline__ u32x4 ring16(const uint8_t* base, uint32_t a, uint32_t mask)
+{
+	const uint32_t a8 = a & ~7u;
+	const uint64_t q0 = *reinterpret_cast<const uint64_t*>(base + (a8 & mask));
+	const uint64_t q1 = *reinterpret_cast<const uint64_t*>(base + ((a8 + 8) & mask));
+	const uint64_t q2 = *reinterpret_cast<const uint64_t*>(base + ((a8 + 16) & mask));
+	const uint32_t w0 = uint32_t(q0), w1 = uint32_t(q0 >> 32), w2 = uint32_t(q1),
+	               w3 = uint32_t(q1 >> 32), w4 = uint32_t(q2), w5 = uint32_t(q2 >> 32);
+	const bool s1 = (a & 4u) != 0;
+	const uint32_t d0 = s1 ? w1 : w0, d1 = s1 ? w2 : w1, d2 = s1 ? w3 : w2, d3 = s1 ? w4 : w3,
+	               d4 = s1 ? w5 : w4;
+	const uint32_t sh = a & 3u;
+	u32x4 v;
+	v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+	v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+	v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+	v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+	return v;
+}
+
 // 16 bytes at block-relative p (literal source): LDS or global.
 __device__ __forceinline__ u32x4 fetch16(const Src& S, int32_t p)
 {
 	if (p >= S.lo && p + 16 <= S.hi)
-		return ld16u(S.lds, uint32_t(p + S.mis) & S.mask, S.mask + 1);
+		return ring16(S.lds, uint32_t(p + S.mis) & S.mask, S.mask);
 	const uintptr_t g = reinterpret_cast<uintptr_t>(S.in) + uintptr_t(intptr_t(p));
 	u32x4 v;
 	if (g + 16 <= S.lim) {
@@ -687,7 +710,7 @@ __device__ __forceinline__ void ostore(DecLds& L, int32_t x, u32x4 v, int32_t n)
 
 __device__ __forceinline__ u32x4 oload16(const DecLds& L, int32_t x)
 {
-	return ld16u(L.oring, uint32_t(x) & OMASK, ORING);
+	return ring16(L.oring, uint32_t(x) & OMASK, OMASK);
 }
 
 // Match with a final source entirely inside the ring (Output_With_History,
