@@ -1309,12 +1309,17 @@ static void exact_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out
 	consumed_total = pos;
 }
 
-// Fast path: every block on its own wavefront.  Returns false when the
-// frame needs the exact path (any block status, checksum mismatch,
-// oversize or short block layouts the slots cannot express).
+// Fast path.  Independent blocks: every block at once (index-driven
+// decoder, two-wave decoder for declined blocks).  Linked frames (blocks
+// of 256 KiB or more, where the reference's Buffer scheme reads exactly the
+// previous block's tail, so the D1 overshoot cannot reach the history):
+// the sequence index of every block at once, then the blocks in order in
+// one workgroup.  Returns false when the frame needs the exact path (any
+// block status, checksum mismatch, a short linked block, oversize or short
+// block layouts the slots cannot express).
 static bool fast_frame(const uint8_t* f, int64_t len, const lz4ada_frame_info& info,
                        const std::vector<lz4ada_block_desc>& descs, uint8_t* out,
-                       int64_t out_cap, int64_t& out_len)
+                       int64_t out_cap, int64_t& out_len, bool linked = false)
 {
 	device_check_or_raise();
 	hipStream_t stream = nullptr;
@@ -1333,8 +1338,12 @@ static bool fast_frame(const uint8_t* f, int64_t len, const lz4ada_frame_info& i
 		                 hipMemcpyHostToDevice));
 		HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
 		HIP_OK(launch_block_checksums(d_frame.p, d_desc.p, nb, d_st.p, stream));
-		HIP_OK(launch_decode_blocks(d_frame.p, uint64_t(info.frame_len), d_desc.p, nb, d_out.p,
-		                            d_st.p, stream));
+		if (linked)
+			HIP_OK(launch_decode_idx(d_frame.p, uint64_t(info.frame_len), d_desc.p, nb, d_out.p,
+			                         d_st.p, stream, 1));
+		else
+			HIP_OK(launch_decode_blocks(d_frame.p, uint64_t(info.frame_len), d_desc.p, nb,
+			                            d_out.p, d_st.p, stream));
 	}
 	std::vector<lz4ada_block_status> st(nb);
 	if (nb)
@@ -1398,9 +1407,10 @@ static void decode_one_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_
 		consumed = info.frame_len;
 		return;
 	}
-	if (indexed && info.format == LZ4ADA_FORMAT_MODERN && info.independent &&
-	    info.frame_len <= len) {
-		if (fast_frame(f, len, info, descs, out, out_cap, out_len)) {
+	if (indexed && info.format == LZ4ADA_FORMAT_MODERN && info.frame_len <= len &&
+	    (info.independent ||
+	     (info.block_max >= (256 << 10) && !getenv("LZ4ADA_NO_FAST_LINKED")))) {
+		if (fast_frame(f, len, info, descs, out, out_cap, out_len, !info.independent)) {
 			consumed = info.frame_len;
 			return;
 		}
@@ -1445,7 +1455,7 @@ int lz4ada_launch_decode_variant(const void* d_frame, uint64_t frame_len,
                                  lz4ada_block_status* d_status, int variant, void* stream)
 {
 	return guarded(nullptr, [&] {
-		if (variant < 0 || variant > 4)
+		if (variant < 0 || variant > 5)
 			raise(LZ4ADA_ASSERTION_ERROR, "unknown decoder variant");
 		HIP_OK(launch_decode_variant(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
 		                             uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,

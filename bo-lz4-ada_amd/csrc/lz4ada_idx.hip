@@ -586,10 +586,11 @@ __device__ __forceinline__ bool next_item(const Src& S, int32_t& p, int32_t& o, 
 // long runs and matches reading the batch itself follow in output order
 // through a leader loop (the first pending item always runs; any other
 // whose source is already final runs with it), with a wave-wide wait
-// between rounds.  Returns false on a reference before the block start.
+// between rounds.  Returns false on a reference before the block start
+// (hb: history bytes before it, linked frames).
 __device__ __forceinline__ bool batch_global(const Src& S, g8* ob, uintptr_t olim, int32_t p0,
                                           int32_t sub_end, int32_t n, int32_t o_lane,
-                                          int32_t o_batch)
+                                          int32_t o_batch, int32_t hb)
 {
 	const int32_t lane = int32_t(lane_id());
 	int32_t cp = 0, co = 0, cpart = 0;
@@ -612,7 +613,7 @@ __device__ __forceinline__ bool batch_global(const Src& S, g8* ob, uintptr_t oli
 			}
 			const int32_t mdst = o + q.L;
 			if (q.ml > 0) {
-				if (q.off > mdst)
+				if (q.off > mdst + hb)
 					pre = true;  // reference before the block start (D2)
 				const int32_t dep_end = mdst - q.off + min(q.off, q.ml);
 				if (q.ml > LONG || dep_end > o_batch) {
@@ -762,21 +763,23 @@ __device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_
 	}
 }
 
-__global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ frame,
-                                                    uint64_t frame_len,
-                                                    const lz4ada_block_desc* __restrict__ desc,
-                                                    uint32_t nblocks, const uint8_t* __restrict__ tab_all,
-                                                    uint8_t* __restrict__ out,
-                                                    lz4ada_block_status* __restrict__ status)
+// One block.  hist: output bytes right before this block's slot that its
+// matches may read -- 0 for independent blocks; in a linked frame, the
+// earlier blocks' output, contiguous when every one of them is full.
+// Returns the block's status code; out_len gets its output length.
+__device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __restrict__ frame,
+                                                uint64_t frame_len,
+                                                const lz4ada_block_desc* __restrict__ desc,
+                                                uint32_t b, const uint8_t* __restrict__ tab_all,
+                                                uint8_t* __restrict__ out,
+                                                lz4ada_block_status* __restrict__ status,
+                                                int64_t hist, int32_t& out_len)
 {
-	__shared__ DecLds D;
-	const uint32_t b = blockIdx.x;
-	if (b >= nblocks)
-		return;
 	const int32_t lane = int32_t(lane_id());
 	const lz4ada_block_desc d = desc[b];
+	out_len = 0;
 	if (status[b].code != DS_OK)
-		return;  // pass 1 declined it
+		return DS_RETRY;  // pass 1 declined it
 	cg8* in = gptr(frame) + d.in_off;
 	g8* ob = gptr(out) + d.out_off;
 	const int32_t n = int32_t(d.in_len);
@@ -801,10 +804,20 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 			status[b].err_out_pos = 0;
 			status[b].out_len = code == DS_OK ? uint32_t(n) : 0u;
 		}
-		return;
+		out_len = code == DS_OK ? n : 0;
+		return code;
 	}
 
 	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+	const int32_t hb = int32_t(min(hist, int64_t(65535)));  // reachable history
+	if (hb > 0) {
+		// the ring's history: the previous block's last bytes
+		for (int32_t x = (-min(hb + 16, ORING - 16)) & ~15; x < 0; x += 64 * 16)
+			if (x + 16 * lane < 0)
+				*reinterpret_cast<u32x4*>(&D.oring[uint32_t(x + 16 * lane) & OMASK]) =
+				    gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(intptr_t(x + 16 * lane)), olim);
+		wave_lds_fence();
+	}
 	cg8* tab = gptr(tab_all) + (((d.in_off >> 8) + b) << 3);
 	const int32_t nsub = (n + SUB - 1) / SUB;
 	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
@@ -893,7 +906,7 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 			if (lane == 0 && o_batch > a0)  // the ring's unflushed tail
 				gstore_n(ob + a0, *reinterpret_cast<const u32x4*>(&D.oring[a0 & OMASK]), o_batch - a0);
 			vm_wait();
-			if (!batch_global(S, ob, olim, p0, sub_end, n, o_lane, o_batch)) {
+			if (!batch_global(S, ob, olim, p0, sub_end, n, o_lane, o_batch, hb)) {
 				bad = true;
 				break;
 			}
@@ -901,10 +914,10 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 			vm_wait();
 			ICOUNT(D_GBATCHES, 1);
 			// reload the ring's history from HBM
-			const int32_t u0 = max(o_batch - ORING + 16, 0) >> 4, u1 = (o_batch + 15) >> 4;
-			for (int32_t u = u0 + lane; u < u1; u += 64)
-				*reinterpret_cast<u32x4*>(&D.oring[(u << 4) & OMASK]) =
-				    gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(u << 4), olim);
+			const int32_t x0 = max(o_batch - ORING + 16, -((hb + 15) & ~15)) & ~15;
+			for (int32_t x = x0 + 16 * lane; x < o_batch + 15; x += 64 * 16)
+				*reinterpret_cast<u32x4*>(&D.oring[uint32_t(x) & OMASK]) =
+				    gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(intptr_t(x)), olim);
 			wave_lds_fence();
 			ISTAMP(D_GLOBAL);
 			k0 += 64;
@@ -955,8 +968,8 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 					o_round += __shfl(inc, 63);
 					const int32_t mdst = rdst[r] + rL[r];
 					if (rml[r] > 0) {
-						if (roff[r] > mdst)
-							pre = true;  // reference before the block start (D2)
+						if (roff[r] > mdst + hb)
+							pre = true;  // reference before the block start (D2) / history
 						if (mdst - roff[r] < glo)
 							anyg = true;
 					}
@@ -1149,6 +1162,49 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 		}
 	}
 	ISTAMP_FLUSH();
+	out_len = bad ? 0 : o_batch;
+	return bad ? DS_RETRY : DS_OK;
+}
+
+// Independent blocks: one wave per block.  Linked frames (linked != 0,
+// launched as one workgroup): the blocks in order, each reading the
+// previous ones' output as history while every block so far is full (its
+// slot then continues the previous one); a declined or short block leaves
+// every later block DS_RETRY for the exact path.
+__global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ frame,
+                                                    uint64_t frame_len,
+                                                    const lz4ada_block_desc* __restrict__ desc,
+                                                    uint32_t nblocks, const uint8_t* __restrict__ tab_all,
+                                                    uint8_t* __restrict__ out,
+                                                    lz4ada_block_status* __restrict__ status,
+                                                    int linked)
+{
+	__shared__ DecLds D;
+	int32_t len;
+	if (!linked) {
+		if (blockIdx.x < nblocks)
+			decode_block(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, 0, len);
+		return;
+	}
+	int64_t hist = 0;
+	uint32_t b = 0;
+	for (; b < nblocks; ++b) {
+		const int32_t code = decode_block(D, frame, frame_len, desc, b, tab_all, out, status,
+		                                  hist, len);
+		vm_wait();  // the next block reads this output as history
+		__syncthreads();
+		if (code != DS_OK)
+			break;
+		if (b + 1 < nblocks && (uint32_t(len) != desc[b].out_cap ||
+		                        desc[b + 1].out_off != desc[b].out_off + uint64_t(len))) {
+			++b;  // the next block's history would not be contiguous
+			break;
+		}
+		hist += len;
+	}
+	for (uint32_t r = b + lane_id(); r < nblocks; r += 64)
+		if (status[r].code == DS_OK || r > b)
+			status[r].code = DS_RETRY;
 }
 
 }  // namespace idx
@@ -1170,7 +1226,7 @@ extern "C" int lz4ada_idx_stamps(unsigned long long* out, int reset)
 
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
                              const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
-                             lz4ada_block_status* d_status, hipStream_t stream)
+                             lz4ada_block_status* d_status, hipStream_t stream, int linked)
 {
 	if (nblocks == 0)
 		return hipSuccess;
@@ -1182,8 +1238,9 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 		return err;
 	hipLaunchKernelGGL(idx::k_index, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len, d_desc,
 	                   nblocks, static_cast<uint8_t*>(tab), d_status);
-	hipLaunchKernelGGL(idx::k_decode_idx, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
-	                   d_desc, nblocks, static_cast<const uint8_t*>(tab), d_out, d_status);
+	hipLaunchKernelGGL(idx::k_decode_idx, dim3(linked ? 1 : nblocks), dim3(64), 0, stream, d_frame,
+	                   frame_len, d_desc, nblocks, static_cast<const uint8_t*>(tab), d_out, d_status,
+	                   linked);
 	err = hipGetLastError();
 	const hipError_t e2 = hipFreeAsync(tab, stream);
 	return err != hipSuccess ? err : e2;

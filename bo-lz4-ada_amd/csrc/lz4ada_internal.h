@@ -52,7 +52,8 @@ struct SerialState {
 // All launch on `stream` and never synchronise.
 
 // Bulk independent-block decoders (LZ4ADA_DECODE_* in lz4ada_hip.h).
-enum DecVariant : int { DEC_PC = 0, DEC_WAVE = 1, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4 };
+enum DecVariant : int { DEC_PC = 0, DEC_WAVE = 1, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4,
+                        DEC_IDX_LINKED = 5 };
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
@@ -73,10 +74,13 @@ hipError_t launch_decode_wg(const uint8_t* d_frame, uint64_t frame_len,
                             lz4ada_block_status* d_status, hipStream_t stream);
 
 // Index-driven decoder alone (lz4ada_idx.hip): k_index + k_decode_idx;
-// declined blocks keep status DS_RETRY and are not decoded.
+// declined blocks keep status DS_RETRY and are not decoded.  linked: the
+// blocks of one linked frame (slots contiguous), decoded in order with the
+// earlier output as history; from the first declined or short block on,
+// every block is left DS_RETRY.
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
                              const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
-                             lz4ada_block_status* d_status, hipStream_t stream);
+                             lz4ada_block_status* d_status, hipStream_t stream, int linked = 0);
 
 // Per-block XXH32 of the compressed payloads (block checksums).
 hipError_t launch_block_checksums(const uint8_t* d_frame,

@@ -2012,6 +2012,8 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 		                   d_desc, nblocks, d_out, d_status, 0);
 		return hipGetLastError();
 	}
+	if (variant == DEC_IDX_LINKED)
+		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream, 1);
 	if (variant == DEC_IDX || variant == DEC_IDX_ALONE) {
 		const hipError_t err = launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out,
 		                                         d_status, stream);

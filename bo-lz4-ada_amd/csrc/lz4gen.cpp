@@ -69,8 +69,10 @@ uint8_t lit_byte(Rng& r, int kind)
 
 }  // namespace
 
-extern "C" int64_t lz4ada_gen_block(int kind, uint64_t seed, uint8_t* raw, int64_t raw_len,
-                                    uint8_t* comp, int64_t comp_cap)
+// hist: bytes raw[-hist .. -1] precede the block (a linked frame's earlier
+// output); offsets may reach back into them.
+static int64_t gen_block(int kind, uint64_t seed, uint8_t* raw, int64_t raw_len, int64_t hist,
+                         uint8_t* comp, int64_t comp_cap)
 {
 	Rng r(seed);
 	Out o{ comp, 0, comp_cap };
@@ -97,7 +99,7 @@ extern "C" int64_t lz4ada_gen_block(int kind, uint64_t seed, uint8_t* raw, int64
 			ml = 4 + r.geo(3.0);
 			break;
 		}
-		if (pos == 0 && L == 0)
+		if (pos == 0 && L == 0 && hist == 0)
 			L = 1;
 		if (pos + L > body)
 			L = body - pos;
@@ -114,7 +116,7 @@ extern "C" int64_t lz4ada_gen_block(int kind, uint64_t seed, uint8_t* raw, int64
 		}
 		pos += L;
 		if (ml) {
-			const int64_t maxoff = pos < 65535 ? pos : 65535;
+			const int64_t maxoff = pos + hist < 65535 ? pos + hist : 65535;
 			if (kind == 2)
 				off = 1;
 			else if (kind == 1 && r.below(4) == 0)
@@ -159,4 +161,18 @@ extern "C" int64_t lz4ada_gen_block(int kind, uint64_t seed, uint8_t* raw, int64
 		}
 	}
 	return o.ok ? o.n : -1;
+}
+
+extern "C" int64_t lz4ada_gen_block(int kind, uint64_t seed, uint8_t* raw, int64_t raw_len,
+                                    uint8_t* comp, int64_t comp_cap)
+{
+	return gen_block(kind, seed, raw, raw_len, 0, comp, comp_cap);
+}
+
+extern "C" int64_t lz4ada_gen_block_linked(int kind, uint64_t seed, uint8_t* buf, int64_t hist,
+                                           int64_t raw_len, uint8_t* comp, int64_t comp_cap)
+{
+	if (!buf || hist < 0)
+		return -1;
+	return gen_block(kind, seed, buf + hist, raw_len, hist, comp, comp_cap);
 }

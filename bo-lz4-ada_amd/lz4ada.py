@@ -193,6 +193,7 @@ _sig = {
     "lz4ada_decode_stream": ([_vp, _i64, _vp, _i64, _pi64], ctypes.c_int),
     "lz4ada_decoded_bound": ([_vp, _i64], _i64),
     "lz4ada_gen_block": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _vp, _i64], _i64),
+    "lz4ada_gen_block_linked": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _i64, _vp, _i64], _i64),
 }
 for _name, (_args, _res) in _sig.items():
     _f = getattr(_lib, _name)
@@ -385,7 +386,7 @@ def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=
                                      stream), _thread_error())
 
 
-DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE = 0, 1, 2, 3, 4
+DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE, DECODE_IDX_LINKED = 0, 1, 2, 3, 4, 5
 
 
 def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,
@@ -430,3 +431,22 @@ def gen_block(kind: int, seed: int, raw_len: int):
     if n < 0:
         raise RuntimeError("gen_block: capacity")
     return comp.raw[:n], raw.raw[:raw_len]
+
+
+def gen_linked_blocks(kind: int, seed: int, block_len: int, nblocks: int, last_len=None):
+    """Blocks of one linked frame whose matches reach back into the earlier
+    blocks' output (up to 64 KiB) -> list of (payload, decoded)."""
+    out, hist = [], b""
+    for i in range(nblocks):
+        raw_len = last_len if (last_len is not None and i == nblocks - 1) else block_len
+        h = hist[-65536:]
+        buf = ctypes.create_string_buffer(h + bytes(max(raw_len, 1)), len(h) + max(raw_len, 1))
+        cap = raw_len + raw_len // 128 + 64 + raw_len // 200 + 1024
+        comp = ctypes.create_string_buffer(cap)
+        n = _lib.lz4ada_gen_block_linked(kind, seed + i, buf, len(h), raw_len, comp, cap)
+        if n < 0:
+            raise RuntimeError("gen_block_linked: capacity")
+        raw = buf.raw[len(h):len(h) + raw_len]
+        out.append((comp.raw[:n], raw))
+        hist += raw
+    return out

@@ -225,6 +225,11 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
  * second step (declined blocks keep status code 10). */
 #define LZ4ADA_DECODE_IDX 3
 #define LZ4ADA_DECODE_IDX_ALONE 4
+/* The blocks of one LINKED frame (slots contiguous, block_max >= 256 KiB):
+ * sequence index of every block at once, then the blocks in order with the
+ * earlier output as history; from the first declined or short block on,
+ * every block is left with status code 10 (the exact path takes over). */
+#define LZ4ADA_DECODE_IDX_LINKED 5
 int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                                  lz4ada_block_status *d_status, int variant, void *stream);
@@ -276,6 +281,11 @@ int lz4ada_abi_version(void);
  */
 int64_t lz4ada_gen_block(int kind, uint64_t seed, uint8_t *raw, int64_t raw_len,
                          uint8_t *comp, int64_t comp_cap);
+/* The same for one block of a linked frame: buf holds `hist` bytes of the
+ * frame's earlier output, then room for raw_len decoded bytes (written at
+ * buf + hist); offsets may reach back into the history (up to 65535). */
+int64_t lz4ada_gen_block_linked(int kind, uint64_t seed, uint8_t *buf, int64_t hist,
+                                int64_t raw_len, uint8_t *comp, int64_t comp_cap);
 
 #ifdef __cplusplus
 }

@@ -456,3 +456,64 @@ def test_idx_decoder_on_vectors(name, digests):
                   for i in range(info.nblocks)]
         if all(s.code == 0 for s in st[:info.nblocks]):
             assert hashlib.sha256(b"".join(pieces)).hexdigest() == digests[name]["sha256"]
+
+
+# ------------------------------------------- linked frames (BASELINE configs[4])
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
+def test_linked_frame_fast_path(kind):
+    """A linked 256 KiB-block frame whose matches reach into the previous
+    block (configs[4] shape, small): the in-order index-driven path decodes
+    every block itself (no decline) and byte-exactly; decode_frame agrees
+    with the oracle."""
+    blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS[kind], 0x4C5A3441, 256 << 10, 6,
+                                      last_len=70000)
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], 256 << 10,
+                                      indep=False, block_cksum=True, content_cksum=True)
+    st_o, ref, _, msg = O.decode_stream(frame)
+    assert st_o == O.OK and ref == raw, msg
+    descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX_LINKED)
+    info, _ = lz4ada.frame_index(frame)
+    assert not info.independent
+    if kind != "literal":  # sparse literal blocks are declined (exact path)
+        assert all(s.code == 0 for s in st[:info.nblocks]), [s.code for s in st[:info.nblocks]]
+    if all(s.code == 0 for s in st[:info.nblocks]):
+        got = b"".join(out[i * info.block_max:i * info.block_max + st[i].out_len]
+                       for i in range(info.nblocks))
+        assert got == raw
+    dec, consumed = lz4ada.decode_frame(frame)
+    assert consumed == len(frame) and dec == raw
+
+
+@pytest.mark.gpu
+def test_linked_frame_short_block_falls_back():
+    """A short middle block breaks the slot layout: the linked path leaves
+    the rest to the exact path, and the frame still decodes exactly."""
+    blocks = lz4ada.gen_linked_blocks(1, 7, 256 << 10, 3)
+    c, r = lz4ada.gen_linked_blocks(1, 8, 5000, 1)[0]  # no history: valid anywhere
+    blocks.insert(1, (c, r))
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], 256 << 10,
+                                      indep=False, block_cksum=True)
+    descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX_LINKED)
+    assert st[0].code == 0 and st[1].code == 0
+    assert all(s.code == lz4ada.DS_RETRY for s in st[2:4])
+    # (the blocks after the inserted one were generated against other
+    # history, so the oracle, not `raw`, says what the frame decodes to)
+    st_o, ref, _, msg = O.decode_stream(frame)
+    assert st_o == O.OK, msg
+    dec, consumed = lz4ada.decode_frame(frame)
+    assert dec == ref
+
+
+@pytest.mark.gpu
+def test_linked_frame_64k_uses_exact_path():
+    """64 KiB linked blocks stay on the exact path (the reference's D1
+    overshoot corner case lives there); output equals the oracle's."""
+    blocks = lz4ada.gen_linked_blocks(1, 11, 64 << 10, 4)
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], 64 << 10,
+                                      indep=False)
+    st_o, ref, _, msg = O.decode_stream(frame)
+    assert st_o == O.OK, msg
+    dec, consumed = lz4ada.decode_frame(frame)
+    assert dec == ref
