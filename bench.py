@@ -142,6 +142,66 @@ def cpu_baseline(recs, block_max, budget_s):
                       "call, block checksums verified)"}
 
 
+def bench_linked(dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, chain=64):
+    """configs[4]: a linked frame (B.Indep = 0) of 4096 x 256 KiB blocks whose
+    matches reach into the previous block: a chain of 64 generated blocks
+    (each against the previous one's output), tiled -- the first block of
+    the chain has no history references, so every tile boundary is valid."""
+    blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS[kind], SEED0, bmax, chain)
+    recs = [lz4frame.block_record(c, stored=False, block_cksum=True) for c, _ in blocks]
+    hashes = [xxhash.xxh32(r).intdigest() for _, r in blocks]
+    order = [i % chain for i in range(nblocks)]
+    offs, pos = [], 0
+    for u in order:
+        offs.append(pos)
+        pos += len(recs[u])
+    d_frame = torch.empty(pos + 64, dtype=torch.uint8, device=dev)
+    d_frame[pos:].zero_()
+    d_rec = [torch.frombuffer(bytearray(r), dtype=torch.uint8).to(dev) for r in recs]
+    descs = (lz4ada.BlockDesc * nblocks)()
+    comp = 0
+    for i, u in enumerate(order):
+        d_frame[offs[i]:offs[i] + len(recs[u])].copy_(d_rec[u])
+        clen = len(blocks[u][0])
+        descs[i].in_off = offs[i] + 4
+        descs[i].in_len = clen
+        descs[i].flags = lz4ada.BLOCK_HAS_CKSUM
+        descs[i].out_off = i * bmax
+        descs[i].out_cap = bmax
+        descs[i].cksum = int.from_bytes(recs[u][4 + clen:8 + clen], "little")
+        comp += clen
+    raw = nblocks * bmax
+    d_desc = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+    d_out = torch.empty(raw, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nblocks * 32, dtype=torch.uint8, device=dev)
+    d_hash = torch.zeros(nblocks, dtype=torch.int32, device=dev)
+    del d_rec
+    run = lambda: lz4ada.launch_decode_variant(d_frame.data_ptr(), pos + 64, d_desc.data_ptr(),
+                                               nblocks, d_out.data_ptr(), d_st.data_ptr(),
+                                               lz4ada.DECODE_IDX_LINKED, sh)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    st = check_statuses(d_st, nblocks)
+    assert all(s.code == 0 for s in st), "linked frame: a block left the fast path"
+    lz4ada.output_checksums_device(d_out.data_ptr(), d_desc.data_ptr(), d_st.data_ptr(), nblocks,
+                                   d_hash.data_ptr(), sh)
+    torch.cuda.synchronize()
+    got = [h & 0xffffffff for h in d_hash.cpu().tolist()]
+    assert got == [hashes[u] for u in order], "linked frame: decoded output differs"
+    del d_frame, d_out
+    return {"workload": f"configs[4]: linked frame (FLG 0x50: B.Checksum, B.Indep=0), {nblocks} x "
+                        f"{bmax >> 10} KiB {kind} blocks, matches reach into the previous block",
+            "decode_ms": round(ms, 3), "MiB_s": round(raw / (ms * 1e-3) / MiB, 1),
+            "compressed_bytes": comp, "decoded_bytes": raw,
+            "path": "k_index (all blocks) + k_decode_idx linked (one workgroup, blocks in order)",
+            "golden": "per-block XXH32 of the output vs the generator"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,6 +215,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--classes", default="", help="extra classes to time, e.g. dense,rle,literal")
+    ap.add_argument("--no-linked", action="store_true",
+                    help="skip the configs[4] row (1 GiB linked frame, 256 KiB blocks)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_decode.json"))
     args = ap.parse_args()
 
@@ -315,6 +377,11 @@ def main():
         del fr, de
     if extra:
         result["classes_decode_kernel"] = extra
+
+    # ---- configs[4]: linked (dependent) 256 KiB-block frame, 1 GiB, one GPU:
+    # the blocks are decoded in order (history carry) by one workgroup
+    if rank == 0 and not args.no_linked:
+        result["linked_c5"] = bench_linked(dev, sh, stream)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(recs, bmax, args.cpu_budget)
