@@ -1180,17 +1180,16 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
                                                     int linked)
 {
 	__shared__ DecLds D;
-	int32_t len;
-	if (!linked) {
-		if (blockIdx.x < nblocks)
-			decode_block(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, 0, len);
-		return;
-	}
+	// one call site of decode_block for both modes (code size)
 	int64_t hist = 0;
-	uint32_t b = 0;
-	for (; b < nblocks; ++b) {
+	uint32_t b = linked ? 0u : blockIdx.x;
+	const uint32_t bend = linked ? nblocks : min(blockIdx.x + 1u, nblocks);
+	for (; b < bend; ++b) {
+		int32_t len;
 		const int32_t code = decode_block(D, frame, frame_len, desc, b, tab_all, out, status,
 		                                  hist, len);
+		if (!linked)
+			return;
 		vm_wait();  // the next block reads this output as history
 		__syncthreads();
 		if (code != DS_OK)
@@ -1202,6 +1201,8 @@ __global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ f
 		}
 		hist += len;
 	}
+	if (!linked)
+		return;
 	for (uint32_t r = b + lane_id(); r < nblocks; r += 64)
 		if (status[r].code == DS_OK || r > b)
 			status[r].code = DS_RETRY;
