@@ -682,7 +682,7 @@ constexpr int OMASK = ORING - 1;
 constexpr int MAXSEQ = 256;     // sequences per batch
 constexpr int RMAX = MAXSEQ / 64;  // rounds of 64 sequences per batch
 constexpr int SLOTS = 12;       // sequence starts in one 32-byte sub-segment (<= 12)
-constexpr int GC = 3;           // 16-byte pieces of an HBM-sourced match loaded ahead
+constexpr int GC = 2;           // 16-byte pieces an HBM-sourced match loads in its own lane
 constexpr int FLUSH_ST = (OW + 15) / 16 / 64 + 1;  // store instructions per flush (fixed)
 static_assert(2 * OW + 16 <= ORING, "batch + its HBM threshold must fit the ring");
 
@@ -691,6 +691,7 @@ struct alignas(16) DecLds {
 	uint8_t oring[ORING];         // output window
 	uint16_t slot[SLOTS][64];     // walk 1: sequence starts of each lane's sub-segment
 	uint16_t cst[MAXSEQ];         // the batch's sequence starts, in order
+	uint8_t own[256];             // piece -> owning lane (dealt HBM pieces)
 };
 
 // Exact-length store of n (1..16) bytes at output position x into the ring.
@@ -982,8 +983,15 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		}
 		ISTAMP(D_WALK2);
 
-		// HBM-sourced matches: every load in flight before the first use
-		u32x4 vg[RMAX][GC];
+		// HBM-sourced matches: every load in flight before the first use.  A
+		// match's first GC pieces load in its own lane; the pieces beyond
+		// (long matches) are dealt over the wave, one per lane and round
+		// (more than 64 in a round: loaded in M, rare).
+		u32x4 vg[RMAX][GC], vr[RMAX];
+		int32_t rtot[RMAX], rpd[RMAX], rpn[RMAX];
+#pragma unroll
+		for (int r = 0; r < RMAX; ++r)
+			rtot[r] = rpd[r] = rpn[r] = 0;
 		if (__any(anyg)) {
 			// the previous batch's flush (FLUSH_ST store instructions) and
 			// the input prefetch (2 loads, when this batch staged) may stay
@@ -1002,6 +1010,28 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					for (int c = 0; c < GC; ++c)
 						if (g && 16 * c < rml[r])
 							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
+					const int32_t nc = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
+					if (__any(nc > 0)) {
+						const int32_t inc = wave_incl_scan(nc);
+						const int32_t excl = inc - nc;
+						rtot[r] = __shfl(inc, 63);
+						for (int32_t k = 0; k < nc; ++k)
+							if (excl + k < 64)
+								D.own[excl + k] = uint8_t(lane);
+						wave_lds_fence();
+						// shuffles with every lane active (ds_bpermute does not
+						// read a lane the EXEC mask has switched off)
+						const int32_t o = D.own[lane] & 63;
+						const int32_t k = GC + lane - __shfl(excl, o);
+						const int32_t osrc = __shfl(src, o);
+						const int32_t od = __shfl(rdst[r] + rL[r], o), oml = __shfl(rml[r], o);
+						if (lane < rtot[r]) {
+							rpd[r] = od + 16 * k;
+							rpn[r] = min(16, oml - 16 * k);
+							__builtin_memcpy(&vr[r], ob + osrc + 16 * k, 16);
+						}
+						wave_lds_fence();  // own[] is dealt again next round
+					}
 				}
 			}
 		}
@@ -1069,24 +1099,23 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #endif
 					}
 				}
-				// pieces of HBM-sourced matches beyond the first GC: dealt over
-				// the wave, so 64 loads are in flight at once
-				{
+				// pieces of HBM-sourced matches beyond the first GC: the first
+				// 64 of the round were loaded in P, dealt over the wave
+				if (rpn[r] > 0)
+					ostore(D, rpd[r], vr[r], rpn[r]);
+				if (rtot[r] > 64) {  // rare: deal the rest now
 					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;
-					if (__any(nc > 0)) {
-						const int32_t inc = wave_incl_scan(nc);
-						const int32_t tot = __shfl(inc, 63);
-						for (int32_t t0 = 0; t0 < tot; t0 += 64) {
-							const int32_t t = t0 + lane;
-							const int32_t lo = piece_owner(inc, t);
-							const int32_t k = GC + t - (__shfl(inc, lo) - __shfl(nc, lo));
-							const int32_t osrc = __shfl(src, lo), odst = __shfl(mdst, lo);
-							const int32_t oml = __shfl(ml, lo);
-							if (t < tot) {
-								u32x4 v;
-								__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
-								ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
-							}
+					const int32_t inc = wave_incl_scan(nc);
+					for (int32_t t0 = 64; t0 < rtot[r]; t0 += 64) {
+						const int32_t t = t0 + lane;
+						const int32_t lo = piece_owner(inc, t);
+						const int32_t k = GC + t - (__shfl(inc, lo) - __shfl(nc, lo));
+						const int32_t osrc = __shfl(src, lo), odst = __shfl(mdst, lo);
+						const int32_t oml = __shfl(ml, lo);
+						if (t < rtot[r]) {
+							u32x4 v;
+							__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
+							ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
 						}
 					}
 				}
