@@ -715,22 +715,42 @@ __device__ __forceinline__ u32x4 oload16(const DecLds& L, int32_t x)
 	return ring16(L.oring, uint32_t(x) & OMASK, OMASK);
 }
 
+// 16 bytes of the period-off sequence whose first off bytes are those of
+// s0|s1 (off < 16), and the store step that keeps its phase: a multiple of
+// off, 9..16 bytes (make_pattern's 8-byte form halves the step for off <= 8).
+__device__ __forceinline__ void make_pattern16(uint64_t s0, uint64_t s1, int32_t off, u32x4& pv,
+                                               int32_t& stp)
+{
+	int32_t width;
+	make_pattern(s0, s1, off, pv, width, stp);
+	if (off <= 8) {
+		// pv holds P[0..7] twice; bytes 8..15 are P[r..r+7], r = 8 mod off
+		const uint64_t x = uint64_t(pv.x) | (uint64_t(pv.y) << 32);
+		const int32_t r = 8 % off;
+		const uint64_t hi = r == 0 ? x : (x >> (8 * r)) | ((x >> (8 * (8 - off))) << (8 * (8 - r)));
+		pv.z = uint32_t(hi);
+		pv.w = uint32_t(hi >> 32);
+		stp = off * (16 / off);
+	}
+}
+
 // Match with a final source entirely inside the ring (Output_With_History,
-// lz4ada.adb:845-904): an off < 16 pattern, else forward 16-byte chunks
-// (a chunk may read bytes the previous chunks of this copy wrote).
+// lz4ada.adb:845-904): an off < 16 pattern stored 9-16 bytes per step (the
+// wave is latency-bound: fewer dependent LDS stores), else forward 16-byte
+// chunks.
 __device__ __forceinline__ void ring_match(DecLds& L, int32_t dst, int32_t off, int32_t len)
 {
 	if (off < 16 && off < len) {
 		const u32x4 s = oload16(L, dst - off);
 		u32x4 pv;
-		int32_t width, stp;
-		make_pattern(uint64_t(s.x) | (uint64_t(s.y) << 32), uint64_t(s.z) | (uint64_t(s.w) << 32),
-		             off, pv, width, stp);
+		int32_t stp;
+		make_pattern16(uint64_t(s.x) | (uint64_t(s.y) << 32), uint64_t(s.z) | (uint64_t(s.w) << 32),
+		               off, pv, stp);
 		for (int32_t k = 0; k < len; k += stp)
-			ostore(L, dst + k, pv, min(width, len - k));
+			ostore(L, dst + k, pv, min(16, len - k));
 		return;
 	}
-	for (int32_t k = 0; k < len; k += 16) {
+	for (int32_t k = 0; k < len; k += 16) {  // a chunk may read what the previous ones wrote
 		const u32x4 v = oload16(L, dst - off + k);
 		wave_lds_fence();
 		ostore(L, dst + k, v, min(16, len - k));
