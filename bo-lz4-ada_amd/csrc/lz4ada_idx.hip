@@ -41,12 +41,10 @@ namespace idx {
 constexpr int SEG = 256;            // pass-1 segment per lane
 constexpr int CHUNK = 64 * SEG;     // pass-1 staged chunk (16 KiB)
 constexpr int SUB = 32;             // pass-2 sub-segment per lane
-constexpr int NSUB = SEG / SUB;     // index bytes per segment
-static_assert(NSUB == 8, "one u64 of index bytes per segment");
+constexpr int NSUB = SEG / SUB;     // index records per segment
 constexpr int BATCH = 64 * SUB;     // pass-2 batch (2 KiB of input)
 constexpr int RING = 4 * BATCH;     // pass-2 staging ring
 constexpr int LONG = 256;           // runs longer than this are copied by the whole wave
-constexpr uint32_t NONE = 0xFFu;
 constexpr int32_t MAX_RUN = 1 << 28;  // length guard (block_max <= 4 MiB in the bulk path)
 
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -301,26 +299,48 @@ struct alignas(16) IdxLds {
 // chain position >= seg_end, or n).  A malformed sequence sets err and
 // returns seg_end as a guess: from a wrong (speculative) entry that is
 // just a dead chain, and a -1 would poison every lane after it one
-// iteration at a time.  ent collects the index bytes of the segment's 8
-// sub-segments.
+// iteration at a time.
+//
+// Every walk rewrites the segment's NSUB index records rec[k] (sub-segment
+// k = bytes [s + 32k, s + 32k + 32)): bit j of the low word = a sequence
+// starts at byte j, the high word = the output bytes (literals + match) of
+// the sequences starting there.  The lane's last walk -- from the true
+// entry -- leaves the exact records.  used counts the sub-segments holding
+// a start.
 __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t s, int32_t seg_end,
-                                                int32_t n, uint64_t& ent, bool& err)
+                                                int32_t n, uint64_t* rec, int32_t& used, bool& err)
 {
-	ent = ~uint64_t(0);
 	err = false;
+	used = 0;
 	int32_t p = e;
+	int32_t kc = -1, nxt = 0;  // sub-segment being counted; next record to write
+	uint32_t bm = 0, cnt = 0;
 	while (p < seg_end) {
-		const uint32_t k = uint32_t(p - s) >> 5;
-		const uint64_t cur = (ent >> (8 * k)) & 0xffu;
-		if (cur == NONE)
-			ent ^= (uint64_t(NONE ^ uint32_t((p - s) & 31)) << (8 * k));
+		const int32_t k = (p - s) >> 5;
+		if (k != kc) {
+			if (kc >= 0)
+				rec[kc] = uint64_t(bm) | (uint64_t(cnt) << 32);
+			for (; nxt < k; ++nxt)
+				if (nxt != kc)
+					rec[nxt] = 0;
+			nxt = k + 1;
+			kc = k;
+			bm = cnt = 0;
+			++used;
+		}
+		bm |= 1u << ((p - s) & 31);
 		Seq q;
 		if (!parse_fast(S, p, n, q)) {
 			err = true;
 			return seg_end;
 		}
+		cnt += uint32_t(q.L + q.ml);
 		p = q.next;
 	}
+	if (kc >= 0)
+		rec[kc] = uint64_t(bm) | (uint64_t(cnt) << 32);
+	for (; nxt < NSUB; ++nxt)
+		rec[nxt] = 0;
 	return p;
 }
 
@@ -356,7 +376,7 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 	const int32_t n = int32_t(d.in_len);
 	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
 	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
-	uint64_t* tab = reinterpret_cast<uint64_t*>(tab_all + (((d.in_off >> 8) + b) << 3));
+	uint64_t* tab = reinterpret_cast<uint64_t*>(tab_all) + (((d.in_off >> 8) + b) << 3);
 
 	Src S;
 	S.lds = X.buf;
@@ -408,9 +428,10 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 		// the true chain, and a run of segments a long sequence jumps over
 		// is crossed in one step instead of one iteration per segment.
 		int32_t ein = (lane == 0) ? E : s;
-		uint64_t ent = ~uint64_t(0);
+		uint64_t* rec = tab + (C >> 5) + NSUB * lane;
+		int32_t used = 0;
 		bool err = false;
-		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, ent, err) : ein;
+		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, rec, used, err) : ein;
 		ISTAMP(I_WALK0);
 		for (int it = 0; it < 64; ++it) {
 			int32_t prev = __shfl_up(wave_incl_max(y), 1);
@@ -423,7 +444,7 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			if (changed) {
 				ein = prev;
 				if (s < n) {
-					y = walk_segment(S, ein, s, seg_end, n, ent, err);
+					y = walk_segment(S, ein, s, seg_end, n, rec, used, err);
 				} else {
 					y = ein;
 					err = false;
@@ -431,12 +452,10 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			}
 		}
 		ISTAMP(I_ITER);
-		// converged: every entry is the true chain position
-		if (s < n) {
-			tab[(C >> 8) + lane] = ent;
-			if (err)
-				bad = true;
-		}
+		// converged: every entry is the true chain position (and every
+		// lane's records are those of its last walk)
+		if (s < n && err)
+			bad = true;
 		bad = __any(bad);
 		E = __shfl(wave_incl_max(y), 63);
 		if (C == 0 && n >= 4 * CHUNK) {
@@ -445,10 +464,6 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			// misses and the entries crawl one lane per iteration -- and are
 			// the one-wave scalar parse's best case: decline the block (large
 			// blocks only: a short one costs a few chunks either way).
-			int32_t used = 0;
-#pragma unroll
-			for (int k = 0; k < NSUB; ++k)
-				used += ((ent >> (8 * k)) & 0xffu) != NONE ? 1 : 0;
 			if (__shfl(wave_incl_scan(used), 63) < CHUNK / SUB / 4)
 				bad = true;
 		}
@@ -681,7 +696,6 @@ constexpr int ORING = 8192;     // LDS output ring (batch + history)
 constexpr int OMASK = ORING - 1;
 constexpr int MAXSEQ = 256;     // sequences per batch
 constexpr int RMAX = MAXSEQ / 64;  // rounds of 64 sequences per batch
-constexpr int SLOTS = 12;       // sequence starts in one 32-byte sub-segment (<= 12)
 constexpr int GC = 2;           // 16-byte pieces an HBM-sourced match loads in its own lane
 constexpr int FLUSH_ST = (OW + 15) / 16 / 64 + 1;  // store instructions per flush (fixed)
 static_assert(2 * OW + 16 <= ORING, "batch + its HBM threshold must fit the ring");
@@ -689,7 +703,6 @@ static_assert(2 * OW + 16 <= ORING, "batch + its HBM threshold must fit the ring
 struct alignas(16) DecLds {
 	uint8_t ring[RING + 16];      // staged input: 4 chunks of 2 KiB (+ mirror)
 	uint8_t oring[ORING];         // output window
-	uint16_t slot[SLOTS][64];     // walk 1: sequence starts of each lane's sub-segment
 	uint16_t cst[MAXSEQ];         // the batch's sequence starts, in order
 	uint8_t own[256];             // piece -> owning lane (dealt HBM pieces)
 };
@@ -839,7 +852,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				    gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(intptr_t(x + 16 * lane)), olim);
 		wave_lds_fence();
 	}
-	cg8* tab = gptr(tab_all) + (((d.in_off >> 8) + b) << 3);
+	const uint64_t* tab = reinterpret_cast<const uint64_t*>(tab_all) + (((d.in_off >> 8) + b) << 3);
 	const int32_t nsub = (n + SUB - 1) / SUB;
 	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
 
@@ -882,32 +895,12 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		const int32_t k = k0 + lane;  // this lane's sub-segment
 		const int32_t sub_s = k * SUB;
 		const int32_t sub_end = min(sub_s + SUB, n);
-		const uint32_t eb = (k < nsub) ? uint32_t(tab[k]) : NONE;
-		const int32_t p0 = (eb == NONE) ? n : sub_s + int32_t(eb);
-
-		// walk 1: output bytes and sequences of this lane
-		int32_t cnt = 0, nseq = 0;
-		bool err = false;
-		for (int32_t p = p0; p < sub_end;) {
-			Seq q;
-			if (!parse_fast(S, p, n, q)) {
-				err = true;
-				break;
-			}
-			cnt += q.L + q.ml;
-			if (nseq < SLOTS)
-				D.slot[nseq][lane] = uint16_t(p - k0 * SUB);
-			++nseq;
-			if (cnt > cap || nseq > SLOTS) {
-				err = true;
-				break;
-			}
-			p = q.next;
-		}
-		if (__any(err)) {
-			bad = true;
-			break;
-		}
+		// this lane's sequence starts and output bytes, from pass 1's record
+		const uint64_t rec = (k < nsub) ? __builtin_nontemporal_load(tab + k) : 0;
+		uint32_t bm = uint32_t(rec);
+		const int32_t cnt = int32_t(min(uint32_t(rec >> 32), 1u << 24));  // > cap: rejected below
+		const int32_t nseq = __popc(bm);
+		const int32_t p0 = bm ? sub_s + __builtin_ctz(bm) : n;
 		const int32_t incl = wave_incl_scan(cnt);
 		const int32_t incl_s = wave_incl_scan(nseq);
 		const int32_t o_lane = o_batch + incl - cnt;
@@ -953,9 +946,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		// the batch's sequence starts, in output order
 		const int32_t base = k0 * SUB;
 		if (lane < m) {
-			const int32_t e0 = incl_s - nseq;
-			for (int32_t j = 0; j < nseq; ++j)
-				D.cst[e0 + j] = D.slot[j][lane];
+			int32_t e = incl_s - nseq;
+			const uint16_t rel = uint16_t(sub_s - base);
+			for (; bm; bm &= bm - 1)
+				D.cst[e++] = uint16_t(rel + __builtin_ctz(bm));
 		}
 		wave_lds_fence();
 		const int32_t N = __shfl(incl_s, m - 1);
@@ -1280,8 +1274,9 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	// index table: 8 bytes per 256-byte segment, per block at ((in_off >> 8) + b) * 8
-	const size_t tab_len = ((size_t(frame_len) >> 8) + size_t(nblocks) + 2) * 8;
+	// index table: 8 records of 8 bytes per 256-byte segment, per block at
+	// record ((in_off >> 8) + b) * 8
+	const size_t tab_len = ((size_t(frame_len) >> 8) + size_t(nblocks) + 2) * 64;
 	void* tab = nullptr;
 	hipError_t err = hipMallocAsync(&tab, tab_len, stream);
 	if (err != hipSuccess)
