@@ -705,6 +705,7 @@ struct alignas(16) DecLds {
 	uint8_t oring[ORING];         // output window
 	uint16_t cst[MAXSEQ];         // the batch's sequence starts, in order
 	uint8_t own[256];             // piece -> owning lane (dealt HBM pieces)
+	uint64_t rrec[4 * 64];        // pass-1 records of the staged chunks' sub-segments
 };
 
 // Exact-length store of n (1..16) bytes at output position x into the ring.
@@ -712,6 +713,9 @@ __device__ __forceinline__ void ostore(DecLds& L, int32_t x, u32x4 v, int32_t n)
 {
 	const uint32_t a = uint32_t(x) & OMASK;
 	if (a + uint32_t(n) <= uint32_t(ORING)) {
+		// one ds_write_b128 even when misaligned: 256 cycles against 1579
+		// for four ds_write_b32 (each misaligned one is split too) and 384
+		// for 16 ds_write_b8 (tools/lds_bench.hip, dependent chain)
 		lds_store_n(&L.oring[a], v, n);
 		return;
 	}
@@ -728,46 +732,89 @@ __device__ __forceinline__ u32x4 oload16(const DecLds& L, int32_t x)
 	return ring16(L.oring, uint32_t(x) & OMASK, OMASK);
 }
 
-// 16 bytes of the period-off sequence whose first off bytes are those of
-// s0|s1 (off < 16), and the store step that keeps its phase: a multiple of
-// off, 9..16 bytes (make_pattern's 8-byte form halves the step for off <= 8).
+// Store steps and phases of period-off patterns without integer division:
+// bits 5(o-1).. = o * (16 / o), bits 40 + 2(o-1).. = 8 mod o, for o = 1..8.
+constexpr uint64_t pattern_lut()
+{
+	uint64_t v = 0;
+	for (int o = 1; o <= 8; ++o)
+		v |= (uint64_t(o * (16 / o)) << (5 * (o - 1))) | (uint64_t(8 % o) << (40 + 2 * (o - 1)));
+	return v;
+}
+constexpr uint64_t PAT_LUT = pattern_lut();
+
+// 16 bytes of the period-off (1..15) sequence whose first off bytes are
+// s0|s1's, and the largest multiple of off <= 16: storing it every stp
+// bytes keeps the phase.
 __device__ __forceinline__ void make_pattern16(uint64_t s0, uint64_t s1, int32_t off, u32x4& pv,
                                                int32_t& stp)
 {
-	int32_t width;
-	make_pattern(s0, s1, off, pv, width, stp);
+	uint64_t x, hi;
 	if (off <= 8) {
-		// pv holds P[0..7] twice; bytes 8..15 are P[r..r+7], r = 8 mod off
-		const uint64_t x = uint64_t(pv.x) | (uint64_t(pv.y) << 32);
-		const int32_t r = 8 % off;
-		const uint64_t hi = r == 0 ? x : (x >> (8 * r)) | ((x >> (8 * (8 - off))) << (8 * (8 - r)));
-		pv.z = uint32_t(hi);
-		pv.w = uint32_t(hi >> 32);
-		stp = off * (16 / off);
+		x = off == 8 ? s0 : (s0 & ((uint64_t(1) << (8 * off)) - 1));
+		for (int32_t w = off; w < 8; w <<= 1)
+			x |= x << (8 * w);
+		const uint32_t sh = uint32_t(off - 1);
+		stp = int32_t((PAT_LUT >> (5 * sh)) & 31u);
+		const int32_t r = int32_t((PAT_LUT >> (40 + 2 * sh)) & 3u);
+		// bytes 8..15: x[r..7], then x from 8 - off on (x is off-periodic)
+		hi = r == 0 ? x : (x >> (8 * r)) | ((x >> (8 * (8 - off))) << (8 * (8 - r)));
+	} else {
+		const int32_t r = off - 8;
+		x = s0;
+		hi = (s1 & ((uint64_t(1) << (8 * r)) - 1)) | (s0 << (8 * r));
+		stp = off;
 	}
+	pv.x = uint32_t(x);
+	pv.y = uint32_t(x >> 32);
+	pv.z = uint32_t(hi);
+	pv.w = uint32_t(hi >> 32);
+}
+
+// a's bytes j < c, b's from c on (c = 1..15)
+__device__ __forceinline__ u32x4 merge_at(u32x4 a, u32x4 b, int32_t c)
+{
+	auto m = [c](int32_t d) -> uint32_t {
+		const int32_t t = c - 4 * d;
+		return t >= 4 ? ~0u : (t <= 0 ? 0u : (1u << (8 * t)) - 1u);
+	};
+	u32x4 v;
+	v.x = (a.x & m(0)) | (b.x & ~m(0));
+	v.y = (a.y & m(1)) | (b.y & ~m(1));
+	v.z = (a.z & m(2)) | (b.z & ~m(2));
+	v.w = (a.w & m(3)) | (b.w & ~m(3));
+	return v;
 }
 
 // Match with a final source entirely inside the ring (Output_With_History,
-// lz4ada.adb:845-904): an off < 16 pattern stored 9-16 bytes per step (the
-// wave is latency-bound: fewer dependent LDS stores), else forward 16-byte
-// chunks.
+// lz4ada.adb:845-904).  Match byte i is source byte i mod off (the overlap
+// rule), so no unit reads this match's own output: an off < 16 overlap
+// stores a 16-byte period pattern every stp bytes, any other match 16
+// source bytes per unit (a unit that wraps the period merges two reads).
+// One loop for both forms: a wave runs max(units) over its lanes, not the
+// two loops one after the other.
 __device__ __forceinline__ void ring_match(DecLds& L, int32_t dst, int32_t off, int32_t len)
 {
-	if (off < 16 && off < len) {
-		const u32x4 s = oload16(L, dst - off);
-		u32x4 pv;
-		int32_t stp;
-		make_pattern16(uint64_t(s.x) | (uint64_t(s.y) << 32), uint64_t(s.z) | (uint64_t(s.w) << 32),
+	const int32_t src = dst - off;
+	u32x4 pv = oload16(L, src);
+	int32_t stp = 16;
+	const bool pat = off < 16 && off < len;
+	if (pat)
+		make_pattern16(uint64_t(pv.x) | (uint64_t(pv.y) << 32), uint64_t(pv.z) | (uint64_t(pv.w) << 32),
 		               off, pv, stp);
-		for (int32_t k = 0; k < len; k += stp)
-			ostore(L, dst + k, pv, min(16, len - k));
-		return;
-	}
-	for (int32_t k = 0; k < len; k += 16) {  // a chunk may read what the previous ones wrote
-		const u32x4 v = oload16(L, dst - off + k);
-		wave_lds_fence();
-		ostore(L, dst + k, v, min(16, len - k));
-		wave_lds_fence();
+	ostore(L, dst, pv, min(16, len));
+	int32_t start = 0;  // unit x of the wide form begins at source byte x mod off
+	for (int32_t x = stp; x < len; x += stp) {
+		u32x4 v = pv;
+		if (!pat) {
+			start += 16;
+			if (start >= off)
+				start -= off;
+			v = oload16(L, src + start);
+			if (off - start < 16)
+				v = merge_at(v, oload16(L, src + start - off), off - start);
+		}
+		ostore(L, dst + x, v, min(16, len - x));
 	}
 }
 
@@ -863,9 +910,17 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 	S.in = in;
 	S.lim = lim;
 
-	int32_t hi = 0;  // input chunks staged: [hi - 4, hi) are in the ring
+	// input chunks staged: [hi - 4, hi) are in the ring, and the records of
+	// sub-segments [64 (hi - 4), 64 hi) in rrec (loaded with the input: a
+	// record load of its own per batch would wait on the previous flush)
+	int32_t hi = 0;
 	u32x4 pf0, pf1;  // chunk hi, loaded ahead
 	load_chunk2(abase, 0, lim, pf0, pf1);
+	auto load_rec = [&](int32_t c) -> uint64_t {
+		const int32_t k = 64 * c + lane;
+		return k < nsub ? __builtin_nontemporal_load(tab + k) : 0;
+	};
+	uint64_t pr = load_rec(0);
 
 	ISTAMP_DECL;
 	int32_t o_batch = 0;  // output position of the current batch
@@ -882,8 +937,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				*reinterpret_cast<u32x4*>(&D.ring[a + 1024 + 16 * lane]) = pf1;
 				if (a == 0 && lane == 0)
 					*reinterpret_cast<u32x4*>(&D.ring[RING]) = pf0;
+				D.rrec[64 * (hi & 3) + lane] = pr;
 				++hi;
 				load_chunk2(abase, hi, lim, pf0, pf1);
+				pr = load_rec(hi);
 			}
 			wave_lds_fence();
 		}
@@ -896,7 +953,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		const int32_t sub_s = k * SUB;
 		const int32_t sub_end = min(sub_s + SUB, n);
 		// this lane's sequence starts and output bytes, from pass 1's record
-		const uint64_t rec = (k < nsub) ? __builtin_nontemporal_load(tab + k) : 0;
+		const uint64_t rec = (k < nsub) ? D.rrec[k & 255] : 0;
 		uint32_t bm = uint32_t(rec);
 		const int32_t cnt = int32_t(min(uint32_t(rec >> 32), 1u << 24));  // > cap: rejected below
 		const int32_t nseq = __popc(bm);
@@ -1008,11 +1065,12 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			rtot[r] = rpd[r] = rpn[r] = 0;
 		if (__any(anyg)) {
 			// the previous batch's flush (FLUSH_ST store instructions) and
-			// the input prefetch (2 loads, when this batch staged) may stay
-			// in flight; everything older -- earlier flushes -- is complete
+			// the input and record prefetch (3 loads, when this batch
+			// staged) may stay in flight; everything older -- earlier
+			// flushes -- is complete
 			static_assert(FLUSH_ST == 4, "update the counted waits");
 			if (staged)
-				asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+				asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
 			else
 				asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
 #pragma unroll
@@ -1213,8 +1271,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 // launched as one workgroup): the blocks in order, each reading the
 // previous ones' output as history while every block so far is full (its
 // slot then continues the previous one); a declined or short block leaves
-// every later block DS_RETRY for the exact path.
-__global__ __launch_bounds__(64) void k_decode_idx(const uint8_t* __restrict__ frame,
+// every later block DS_RETRY for the exact path.  Pinned to two waves per
+// SIMD (256 registers): past that the allocator reaches for AGPRs and the
+// bench's 2048 blocks would no longer be resident at once.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_idx(const uint8_t* __restrict__ frame,
                                                     uint64_t frame_len,
                                                     const lz4ada_block_desc* __restrict__ desc,
                                                     uint32_t nblocks, const uint8_t* __restrict__ tab_all,

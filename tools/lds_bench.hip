@@ -86,6 +86,11 @@ __global__ __launch_bounds__(512) void k(uint32_t* out, uint32_t seed, int iters
 			for (int j = 0; j < 16; ++j)
 				buf[a + j] = uint8_t(x >> j);
 			acc += buf[a + 3];
+		} else if (MODE == 10) {  // 16-byte store as 4 ds_write_b32 at any alignment
+			const uint32_t la = uint32_t(reinterpret_cast<uintptr_t>(buf + a));
+			asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %0, %2 offset:4\n\tds_write_b32 %0, %3 offset:8\n\tds_write_b32 %0, %4 offset:12"
+			             ::"v"(la), "v"(x), "v"(x + 1), "v"(x + 2), "v"(x + 3) : "memory");
+			acc += buf[a + 3];
 		} else if (MODE == 5) {  // aligned b128 store
 			u32x4 v = {x, x + 1, x + 2, x + 3};
 			*reinterpret_cast<u32x4*>(buf + (a & ~15u)) = v;
@@ -104,9 +109,9 @@ int main()
 	unsigned long long* cyc;
 	hipMalloc(&out, 256 * 2 * 512 * 4);
 	hipMalloc(&cyc, 8);
-	const char* names[] = {"u8", "b128 aligned", "b128 unaligned (memcpy)", "2x b64 + shift", "st b128 unaligned + u8", "st b128 aligned + u8", "2x b128 aligned + funnel", "16x u8 reads", "st 16B aligned pieces + u8", "st 16x b8 + u8"};
+	const char* names[] = {"u8", "b128 aligned", "b128 unaligned (memcpy)", "2x b64 + shift", "st b128 unaligned + u8", "st b128 aligned + u8", "2x b128 aligned + funnel", "16x u8 reads", "st 16B aligned pieces + u8", "st 16x b8 + u8", "st 4x b32 any-align + u8"};
 	const int iters = 4096;
-	for (int m = 0; m < 10; ++m) {
+	for (int m = 0; m < 11; ++m) {
 		for (int rep = 0; rep < 2; ++rep) {
 			hipMemset(cyc, 0, 8);
 			hipEvent_t e0, e1;
@@ -124,6 +129,7 @@ int main()
 			case 7: hipLaunchKernelGGL(k<7>, dim3(256), dim3(512), 0, 0, out, 1u, iters, cyc); break;
 			case 8: hipLaunchKernelGGL(k<8>, dim3(256), dim3(512), 0, 0, out, 1u, iters, cyc); break;
 			case 9: hipLaunchKernelGGL(k<9>, dim3(256), dim3(512), 0, 0, out, 1u, iters, cyc); break;
+			case 10: hipLaunchKernelGGL(k<10>, dim3(256), dim3(512), 0, 0, out, 1u, iters, cyc); break;
 			}
 			hipEventRecord(e1);
 			hipEventSynchronize(e1);
