@@ -291,7 +291,9 @@ __device__ __forceinline__ void gstore_n(g8* dst, u32x4 v, int32_t n)
 // ------------------------------------------------------------------ pass 1
 
 struct alignas(16) IdxLds {
-	uint8_t buf[CHUNK + 16];  // staged chunk; + mirror of its first 16 bytes
+	uint8_t buf[CHUNK + 16];       // staged chunk; + mirror of its first 16 bytes
+	uint32_t rbm[64][NSUB + 1];    // each lane's records from its latest walk: start
+	uint16_t rcnt[64][NSUB + 1];   // bitmaps and output bytes (>= 0xFFFF: in HBM)
 };
 
 // Walk the chain from e (an entry at or after this lane's segment start s)
@@ -301,17 +303,25 @@ struct alignas(16) IdxLds {
 // just a dead chain, and a -1 would poison every lane after it one
 // iteration at a time.
 //
-// Every walk rewrites the segment's NSUB index records rec[k] (sub-segment
-// k = bytes [s + 32k, s + 32k + 32)): bit j of the low word = a sequence
-// starts at byte j, the high word = the output bytes (literals + match) of
-// the sequences starting there.  The lane's last walk -- from the true
-// entry -- leaves the exact records.  used counts the sub-segments holding
-// a start.
+// Every walk rewrites the segment's NSUB records (sub-segment k = bytes
+// [s + 32k, s + 32k + 32)) in LDS: rb[k] bit j = a sequence starts at byte
+// j, rc[k] = the output bytes (literals + match) of the sequences starting
+// there.  The lane's last walk -- from the true entry -- leaves the exact
+// records; k_index writes them to HBM once per chunk.  An output count that
+// does not fit 16 bits goes straight to its record's high word in HBM
+// (ghi[2k]; long RLE runs).  used counts the sub-segments holding a start.
 __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t s, int32_t seg_end,
-                                                int32_t n, uint64_t* rec, int32_t& used, bool& err)
+                                                int32_t n, uint32_t* rb, uint16_t* rc, uint32_t* ghi,
+                                                int32_t& used, bool& err)
 {
 	err = false;
 	used = 0;
+	auto put = [&](int32_t k, uint32_t b, uint32_t c) {
+		rb[k] = b;
+		rc[k] = uint16_t(min(c, 0xFFFFu));
+		if (c >= 0xFFFFu)
+			ghi[2 * k] = c;
+	};
 	int32_t p = e;
 	int32_t kc = -1, nxt = 0;  // sub-segment being counted; next record to write
 	uint32_t bm = 0, cnt = 0;
@@ -319,10 +329,10 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 		const int32_t k = (p - s) >> 5;
 		if (k != kc) {
 			if (kc >= 0)
-				rec[kc] = uint64_t(bm) | (uint64_t(cnt) << 32);
+				put(kc, bm, cnt);
 			for (; nxt < k; ++nxt)
 				if (nxt != kc)
-					rec[nxt] = 0;
+					put(nxt, 0, 0);
 			nxt = k + 1;
 			kc = k;
 			bm = cnt = 0;
@@ -338,9 +348,9 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 		p = q.next;
 	}
 	if (kc >= 0)
-		rec[kc] = uint64_t(bm) | (uint64_t(cnt) << 32);
+		put(kc, bm, cnt);
 	for (; nxt < NSUB; ++nxt)
-		rec[nxt] = 0;
+		put(nxt, 0, 0);
 	return p;
 }
 
@@ -428,10 +438,11 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 		// the true chain, and a run of segments a long sequence jumps over
 		// is crossed in one step instead of one iteration per segment.
 		int32_t ein = (lane == 0) ? E : s;
-		uint64_t* rec = tab + (C >> 5) + NSUB * lane;
+		uint32_t* ghi = reinterpret_cast<uint32_t*>(tab + (C >> 5) + NSUB * lane) + 1;
 		int32_t used = 0;
 		bool err = false;
-		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, rec, used, err) : ein;
+		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used, err)
+		                    : ein;
 		ISTAMP(I_WALK0);
 		for (int it = 0; it < 64; ++it) {
 			int32_t prev = __shfl_up(wave_incl_max(y), 1);
@@ -444,7 +455,7 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			if (changed) {
 				ein = prev;
 				if (s < n) {
-					y = walk_segment(S, ein, s, seg_end, n, rec, used, err);
+					y = walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used, err);
 				} else {
 					y = ein;
 					err = false;
@@ -452,11 +463,23 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			}
 		}
 		ISTAMP(I_ITER);
-		// converged: every entry is the true chain position (and every
-		// lane's records are those of its last walk)
+		// converged: every entry is the true chain position, and every
+		// lane's records are those of its last walk: to HBM, coalesced
 		if (s < n && err)
 			bad = true;
 		bad = __any(bad);
+		wave_lds_fence();
+#pragma unroll
+		for (int i = 0; i < NSUB; ++i) {
+			const int32_t r = 64 * i + lane, sg = r >> 3, sb = r & (NSUB - 1);
+			if (C + SEG * sg < n) {
+				const uint32_t bmv = X.rbm[sg][sb], c16 = X.rcnt[sg][sb];
+				if (c16 != 0xFFFFu)
+					tab[(C >> 5) + r] = uint64_t(bmv) | (uint64_t(c16) << 32);
+				else  // the exact count is in the high word already
+					*reinterpret_cast<uint32_t*>(tab + (C >> 5) + r) = bmv;
+			}
+		}
 		E = __shfl(wave_incl_max(y), 63);
 		if (C == 0 && n >= 4 * CHUNK) {
 			// Sparse chains (over 64 input bytes per sequence: long literal
