@@ -101,6 +101,47 @@ def build_shard(recs, first_block, nblocks, block_max, dev):
     return d_frame, frame_len, d_desc, exp_hash, comp_bytes, raw_bytes, descs
 
 
+def cpu_baseline_parallel(recs, block_max, threads, blocks_per_thread):
+    """SURVEY §8d's N-core extrapolation for independent frames: `threads`
+    threads, each running the oracle's unlz4ada loop (ctypes releases the
+    GIL) over its own frame of `blocks_per_thread` independent blocks of the
+    same workload.  Reported beside cpu_baseline, never as it."""
+    import concurrent.futures
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    frames = []
+    for t in range(threads):
+        blocks = [(recs[(t * blocks_per_thread + i) % len(recs)][4],
+                   recs[(t * blocks_per_thread + i) % len(recs)][5], False)
+                  for i in range(blocks_per_thread)]
+        frames.append(lz4frame.build_frame(blocks, block_max, indep=True, block_cksum=True))
+
+    L = O.lib()
+    # output buffers and expected hashes outside the timed region; inside it
+    # only the C loop runs (ctypes drops the GIL for the call)
+    outs = [ctypes.create_string_buffer(len(raw) + MiB) for _, raw in frames]
+    want = [xxhash.xxh32(raw).intdigest() for _, raw in frames]
+    lens = [ctypes.c_int64() for _ in frames]
+
+    def run(t):
+        data, raw = frames[t]
+        err = ctypes.create_string_buffer(512)
+        st = L.oracle_unlz4ada(data, len(data), outs[t], len(raw) + MiB, ctypes.byref(lens[t]), err, 512)
+        assert st == O.OK and lens[t].value == len(raw), err.value
+        return len(raw)
+
+    with concurrent.futures.ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        total = sum(ex.map(run, range(threads)))
+        dt = time.perf_counter() - t0
+    for t in range(threads):
+        assert L.oracle_xxh32_hash(outs[t], lens[t].value) == want[t], "oracle output differs"
+    return {"value": round(total / dt / MiB, 1), "unit": "MiB/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x {blocks_per_thread} x 4 MiB blocks ({total / MiB:.0f} MiB "
+                      f"decoded, {dt:.1f} s), one frame per thread through the oracle's unlz4ada "
+                      "loop; block-parallel extrapolation for independent frames (SURVEY §8d)"}
+
+
 def content_hash(recs, nblocks):
     """Expected frame-wide XXH32 of rank 0's decoded shard (python-xxhash over
     the generator's plaintext, tiled like build_shard)."""
@@ -124,17 +165,26 @@ def cpu_baseline(recs, block_max, budget_s):
     def frame_of(k):
         blocks = [(recs[i % len(recs)][4], recs[i % len(recs)][5], False) for i in range(k)]
         return lz4frame.build_frame(blocks, block_max, indep=True, block_cksum=True)
+    L = O.lib()
+
+    def timed(frame, raw):
+        # the C loop alone: output buffer allocated, and the output checked,
+        # outside the timed call
+        out = ctypes.create_string_buffer(len(raw) + MiB)
+        n = ctypes.c_int64()
+        err = ctypes.create_string_buffer(512)
+        t0 = time.perf_counter()
+        st = L.oracle_unlz4ada(frame, len(frame), out, len(raw) + MiB, ctypes.byref(n), err, 512)
+        dt = time.perf_counter() - t0
+        assert st == O.OK and n.value == len(raw), err.value
+        assert L.oracle_xxh32_hash(out, n.value) == xxhash.xxh32(raw).intdigest()
+        return dt
+
     f1, raw1 = frame_of(1)
-    t0 = time.perf_counter()
-    st, out, msg = O.unlz4ada(f1, out_cap=len(raw1) + MiB)
-    t1 = time.perf_counter() - t0
-    assert st == O.OK and out == raw1, msg
+    t1 = timed(f1, raw1)
     k = max(1, min(2048, int(budget_s / max(t1, 1e-6))))
     fk, rawk = frame_of(k)
-    t0 = time.perf_counter()
-    st, out, msg = O.unlz4ada(fk, out_cap=len(rawk) + MiB)
-    dt = time.perf_counter() - t0
-    assert st == O.OK and len(out) == len(rawk), msg
+    dt = timed(fk, rawk)
     return {"value": round(len(rawk) / dt / MiB, 1), "unit": "MiB/s", "cores": 1,
             "kind": "port",
             "sample": f"{k} x 4 MiB blocks ({len(rawk) / MiB:.0f} MiB decoded, {dt:.1f} s) of the "
@@ -385,6 +435,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(recs, bmax, args.cpu_budget)
+        threads = min(16, os.cpu_count() or 1)
+        result["cpu_baseline_parallel"] = cpu_baseline_parallel(recs, bmax, threads, 64)
     elif rank == 0:
         result["cpu_baseline"] = None
 
