@@ -717,9 +717,9 @@ __device__ __forceinline__ bool batch_global(const Src& S, g8* ob, uintptr_t oli
 constexpr int OW = 4080;        // max batch output assembled in LDS (see glo below)
 constexpr int ORING = 8192;     // LDS output ring (batch + history)
 constexpr int OMASK = ORING - 1;
-constexpr int MAXSEQ = 256;     // sequences per batch
+constexpr int MAXSEQ = 128;     // sequences per batch (2 rounds: 192 VGPRs; 256 took 254 and spilled)
 constexpr int RMAX = MAXSEQ / 64;  // rounds of 64 sequences per batch
-constexpr int GC = 2;           // 16-byte pieces an HBM-sourced match loads in its own lane
+constexpr int GC = 1;           // 16-byte pieces an HBM-sourced match loads in its own lane (1: fewest registers; the rest are dealt)
 constexpr int FLUSH_ST = (OW + 15) / 16 / 64 + 1;  // store instructions per flush (fixed)
 static_assert(2 * OW + 16 <= ORING, "batch + its HBM threshold must fit the ring");
 
@@ -1295,8 +1295,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 // previous ones' output as history while every block so far is full (its
 // slot then continues the previous one); a declined or short block leaves
 // every later block DS_RETRY for the exact path.  Pinned to two waves per
-// SIMD (256 registers): past that the allocator reaches for AGPRs and the
-// bench's 2048 blocks would no longer be resident at once.
+// SIMD (at most 256 registers, so the allocator never reaches for AGPRs):
+// LDS allows 8 waves per CU, and the bench's 2048 blocks are all resident.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_idx(const uint8_t* __restrict__ frame,
                                                     uint64_t frame_len,
                                                     const lz4ada_block_desc* __restrict__ desc,
