@@ -1091,11 +1091,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			// the input and record prefetch (3 loads, when this batch
 			// staged) may stay in flight; everything older -- earlier
 			// flushes -- is complete
-			static_assert(FLUSH_ST == 4, "update the counted waits");
 			if (staged)
-				asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+				asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FLUSH_ST + 3) : "memory");
 			else
-				asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+				asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FLUSH_ST) : "memory");
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
 				if (64 * r < N) {
