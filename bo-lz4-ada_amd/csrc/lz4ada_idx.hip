@@ -397,19 +397,19 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 
 	// 16 KiB chunk at aligned address a (lanes: 16 x 16 bytes each), the
 	// next one loaded while the current one is walked
-	auto load16k = [&](uintptr_t a, u32x4 (&v)[16]) {
+	auto load16k = [&](uintptr_t a, u32x4 (&v)[CHUNK / 1024]) {
 		if (a + CHUNK <= lim) {
 #pragma unroll
-			for (int r = 0; r < 16; ++r)
+			for (int r = 0; r < CHUNK / 1024; ++r)
 				__builtin_memcpy(&v[r], reinterpret_cast<cg8*>(a + uintptr_t(1024 * r + 16 * lane)), 16);
 		} else {
 #pragma unroll
-			for (int r = 0; r < 16; ++r)
+			for (int r = 0; r < CHUNK / 1024; ++r)
 				v[r] = gload16(a + uintptr_t(1024 * r + 16 * lane), lim);
 		}
 	};
 	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
-	u32x4 pf[16];
+	u32x4 pf[CHUNK / 1024];
 	if (n > 0)
 		load16k(abase, pf);
 
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 	for (int32_t C = 0; C < n && !bad; C += CHUNK) {
 		// stage block-relative [C - mis, C - mis + CHUNK) (16-byte aligned addresses)
 #pragma unroll
-		for (int r = 0; r < 16; ++r)
+		for (int r = 0; r < CHUNK / 1024; ++r)
 			*reinterpret_cast<u32x4*>(&X.buf[1024 * r + 16 * lane]) = pf[r];
 		if (lane == 0)
 			*reinterpret_cast<u32x4*>(&X.buf[CHUNK]) = pf[0];
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 		wave_lds_fence();
 #pragma unroll
 		for (int i = 0; i < NSUB; ++i) {
-			const int32_t r = 64 * i + lane, sg = r >> 3, sb = r & (NSUB - 1);
+			const int32_t r = 64 * i + lane, sg = r / NSUB, sb = r & (NSUB - 1);
 			if (C + SEG * sg < n) {
 				const uint32_t bmv = X.rbm[sg][sb], c16 = X.rcnt[sg][sb];
 				if (c16 != 0xFFFFu)
