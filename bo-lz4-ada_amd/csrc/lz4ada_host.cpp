@@ -14,6 +14,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -941,8 +942,9 @@ const char* lz4ada_error_name(int status)
 		                             "LZ4ADA.TOO_LITTLE_MEMORY",
 		                             "ADA.ASSERTIONS.ASSERTION_ERROR",
 		                             "CONSTRAINT_ERROR",
-		                             "LZ4ADA.DEVICE_ERROR" };
-	if (status < 0 || status > LZ4ADA_DEVICE_ERROR)
+		                             "LZ4ADA.DEVICE_ERROR",
+		                             "LZ4ADA.EXACT_PATH" };
+	if (status < 0 || status > LZ4ADA_EXACT_PATH)
 		return "UNKNOWN";
 	return names[status];
 }
@@ -1272,10 +1274,34 @@ static void index_frame(const uint8_t* f, int64_t len, lz4ada_frame_info& info,
 	info.frame_len = pos;
 }
 
+// Where decoded bytes go: the caller's fixed buffer, or a malloc'd buffer
+// that grows (lz4ada_decode_*_alloc).  `len` is what is committed so far.
+struct Sink {
+	uint8_t* p = nullptr;
+	int64_t cap = 0;
+	bool growable = false;
+	int64_t len = 0;
+	// Room for n more bytes after len.
+	uint8_t* room(int64_t n)
+	{
+		if (len + n > cap) {
+			if (!growable)
+				raise(LZ4ADA_CONSTRAINT_ERROR, "output capacity exceeded");
+			int64_t c = std::max<int64_t>(len + n, std::max<int64_t>(2 * cap, 1 << 16));
+			void* q = realloc(p, size_t(c));
+			if (!q)
+				raise(LZ4ADA_CONSTRAINT_ERROR, "output allocation failed");
+			p = static_cast<uint8_t*>(q);
+			cap = c;
+		}
+		return p + len;
+	}
+	void commit(int64_t n) { len += n; }
+};
+
 // Reference-exact path for one frame: the unlz4ada loop
 // (tool_unlz4ada/unlz4ada.adb:84-103) over the streaming engine.
-static void exact_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out_cap,
-                        int64_t& out_len, int64_t& consumed_total)
+static void exact_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& consumed_total)
 {
 	int64_t consumed = 0, mbs = 0;
 	lz4ada_decompressor* raw = nullptr;
@@ -1284,7 +1310,6 @@ static void exact_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out
 		raise(st, g_thread_error);
 	std::unique_ptr<lz4ada_decompressor> ctx(raw);
 	std::vector<uint8_t> buf(size_t(mbs), 0);
-	out_len = 0;
 	int eof = LZ4ADA_EOF_NO;
 	int64_t pos = consumed;
 	while (pos < len) {
@@ -1292,10 +1317,8 @@ static void exact_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out
 		ctx->update(f + pos, len - pos, c, buf.data(), mbs, first, last);
 		if (last >= first) {
 			const int64_t nout = last - first + 1;
-			if (out_len + nout > out_cap)
-				raise(LZ4ADA_CONSTRAINT_ERROR, "output capacity exceeded");
-			memcpy(out + out_len, buf.data() + first, size_t(nout));
-			out_len += nout;
+			memcpy(out.room(nout), buf.data() + first, size_t(nout));
+			out.commit(nout);
 		}
 		pos += c;
 		eof = ctx->is_end_of_frame();
@@ -1309,90 +1332,313 @@ static void exact_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out
 	consumed_total = pos;
 }
 
-// Fast path.  Independent blocks: every block at once (index-driven
-// decoder, two-wave decoder for declined blocks).  Linked frames (blocks
-// of 256 KiB or more, where the reference's Buffer scheme reads exactly the
-// previous block's tail, so the D1 overshoot cannot reach the history):
-// the sequence index of every block at once, then the blocks in order in
-// one workgroup.  Returns false when the frame needs the exact path (any
-// block status, checksum mismatch, a short linked block, oversize or short
-// block layouts the slots cannot express).
-static bool fast_frame(const uint8_t* f, int64_t len, const lz4ada_frame_info& info,
-                       const std::vector<lz4ada_block_desc>& descs, uint8_t* out,
-                       int64_t out_cap, int64_t& out_len, bool linked = false)
+// A device allocation that may fail without raising (the bulk path then
+// shrinks its batch or hands the frame to the exact path).
+template <class T>
+static bool try_reserve(DevBuf<T>& b, size_t count)
 {
-	device_check_or_raise();
-	hipStream_t stream = nullptr;
-	const uint32_t nb = uint32_t(descs.size());
-	DevBuf<uint8_t> d_frame, d_out;
-	DevBuf<lz4ada_block_desc> d_desc;
-	DevBuf<lz4ada_block_status> d_st;
-	d_frame.reserve(size_t(info.frame_len));
-	HIP_OK(hipMemcpy(d_frame.p, f, size_t(info.frame_len), hipMemcpyHostToDevice));
-	const uint64_t slots = uint64_t(std::max<uint32_t>(nb, 1)) * uint64_t(info.block_max);
-	d_out.reserve(size_t(slots));
-	d_desc.reserve(std::max<uint32_t>(nb, 1));
-	d_st.reserve(std::max<uint32_t>(nb, 1));
-	if (nb) {
-		HIP_OK(hipMemcpy(d_desc.p, descs.data(), nb * sizeof(lz4ada_block_desc),
-		                 hipMemcpyHostToDevice));
-		HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
-		HIP_OK(launch_block_checksums(d_frame.p, d_desc.p, nb, d_st.p, stream));
-		if (linked)
-			HIP_OK(launch_decode_idx(d_frame.p, uint64_t(info.frame_len), d_desc.p, nb, d_out.p,
-			                         d_st.p, stream, 1));
-		else
-			HIP_OK(launch_decode_blocks(d_frame.p, uint64_t(info.frame_len), d_desc.p, nb,
-			                            d_out.p, d_st.p, stream));
-	}
-	std::vector<lz4ada_block_status> st(nb);
-	if (nb)
-		HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status),
-		                 hipMemcpyDeviceToHost));
-	uint64_t total = 0;
-	bool contiguous = true;
-	std::vector<uint64_t> dst_off(nb);
-	for (uint32_t i = 0; i < nb; ++i) {
-		if (st[i].code != DS_OK)
-			return false;
-		if ((descs[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != descs[i].cksum)
-			return false;
-		dst_off[i] = total;
-		if (total != descs[i].out_off)
-			contiguous = false;
-		total += st[i].out_len;
-	}
-	if (info.has_content_size && total != info.content_size)
+	if (count <= b.n && b.p)
+		return true;
+	b.release();
+	if (hipMalloc(reinterpret_cast<void**>(&b.p), std::max<size_t>(count, 1) * sizeof(T) + 64) !=
+	    hipSuccess) {
+		(void)hipGetLastError();
+		b.p = nullptr;
 		return false;
-	if (int64_t(total) > out_cap)
-		raise(LZ4ADA_CONSTRAINT_ERROR, "output capacity exceeded");
-	const uint8_t* d_res = d_out.p;
-	DevBuf<uint8_t> d_compact;
-	if (!contiguous) {
-		DevBuf<uint64_t> d_off;
-		d_off.reserve(nb);
-		d_compact.reserve(size_t(std::max<uint64_t>(total, 1)));
-		HIP_OK(hipMemcpy(d_off.p, dst_off.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice));
-		HIP_OK(launch_compact(d_out.p, d_desc.p, d_off.p, d_st.p, nb, d_compact.p, stream));
-		HIP_OK(hipDeviceSynchronize());
-		d_res = d_compact.p;
 	}
-	if (info.content_checksum) {
-		// D2H overlapped with the host XXH32 chain (content_xxh32_d2h)
-		lz4ada_xxh32_state h;
-		lz4ada_xxh32_reset(&h, 0);
-		content_xxh32_d2h(h, d_res, int64_t(total), out, stream);
-		if (h.hash != info.content_checksum_declared)
-			return false;
-	} else if (total) {
-		HIP_OK(hipMemcpy(out, d_res, size_t(total), hipMemcpyDeviceToHost));
-	}
-	out_len = int64_t(total);
+	b.n = count;
 	return true;
 }
 
-static void decode_one_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_t out_cap,
-                             int64_t& out_len, int64_t& consumed)
+static int64_t env_bytes(const char* name, int64_t dflt)
+{
+	const char* e = getenv(name);
+	if (!e || !*e)
+		return dflt;
+	const long long v = atoll(e);
+	return v > 0 ? int64_t(v) : dflt;
+}
+
+// Output slot capacity of one block: a stored block is its payload; a
+// compressed one decodes to at most 255 bytes per payload byte (a length
+// extension byte adds <= 255 to a match; everything else expands less), so
+// a frame of many small flushed blocks does not reserve block_max each.
+static uint32_t slot_cap(const lz4ada_block_desc& d, int64_t bmax)
+{
+	if (d.flags & LZ4ADA_BLOCK_STORED)
+		return d.in_len;
+	return uint32_t(std::min<uint64_t>(uint64_t(bmax), 255ull * d.in_len + 64));
+}
+
+static uint64_t round256(uint64_t v) { return (v + 255) & ~uint64_t(255); }
+
+// Contiguous runs of blocks [lo, hi) whose slot bytes (plus `extra` per
+// block) stay within `budget` (at least one block each).
+static std::vector<std::pair<uint32_t, uint32_t>> batches_of(const std::vector<lz4ada_block_desc>& descs,
+                                                             int64_t bmax, uint64_t extra,
+                                                             uint64_t budget)
+{
+	std::vector<std::pair<uint32_t, uint32_t>> v;
+	uint32_t lo = 0;
+	uint64_t acc = 0;
+	for (uint32_t i = 0; i < descs.size(); ++i) {
+		const uint64_t need = round256(slot_cap(descs[i], bmax)) + extra;
+		if (i > lo && acc + need > budget) {
+			v.emplace_back(lo, i);
+			lo = i;
+			acc = 0;
+		}
+		acc += need;
+	}
+	if (lo < descs.size())
+		v.emplace_back(lo, uint32_t(descs.size()));
+	return v;
+}
+
+enum BulkResult { BULK_OK, BULK_EXACT, BULK_PRE_REF };
+
+// Independent blocks, batch by batch: block checksums + the bulk decoder
+// over slots, then the batch's bytes (compacted if a block is short) to the
+// sink, hashed on the way when the frame has a content checksum.
+static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_info& info,
+                                   const std::vector<lz4ada_block_desc>& descs, Sink& out,
+                                   lz4ada_xxh32_state* h, uint64_t& total)
+{
+	hipStream_t stream = nullptr;
+	uint64_t budget = uint64_t(env_bytes("LZ4ADA_BATCH_BYTES", int64_t(4) << 30));
+	uint32_t lo = 0;
+	total = 0;
+	while (lo < descs.size()) {
+		const auto bt = batches_of(std::vector<lz4ada_block_desc>(descs.begin() + lo, descs.end()),
+		                           info.block_max, 0, budget);
+		const uint32_t hi = lo + bt[0].second;
+		const uint32_t nb = hi - lo;
+		std::vector<lz4ada_block_desc> d(descs.begin() + lo, descs.begin() + hi);
+		uint64_t slots = 0;
+		for (auto& x : d) {
+			x.out_cap = slot_cap(x, info.block_max);
+			x.out_off = slots;
+			slots += round256(x.out_cap);
+		}
+		DevBuf<uint8_t> d_out, d_compact;
+		DevBuf<lz4ada_block_desc> d_desc;
+		DevBuf<lz4ada_block_status> d_st;
+		if (!try_reserve(d_out, size_t(slots))) {
+			if (budget > (uint64_t(64) << 20) && nb > 1) {
+				budget /= 2;  // retry this batch smaller
+				continue;
+			}
+			return BULK_EXACT;
+		}
+		d_desc.reserve(nb);
+		d_st.reserve(nb);
+		HIP_OK(hipMemcpy(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc), hipMemcpyHostToDevice));
+		HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
+		HIP_OK(launch_block_checksums(d_frame, d_desc.p, nb, d_st.p, stream));
+		HIP_OK(launch_decode_blocks(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out.p, d_st.p,
+		                            stream));
+		std::vector<lz4ada_block_status> st(nb);
+		HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status), hipMemcpyDeviceToHost));
+		bool pre = false;
+		uint64_t bt_total = 0;
+		bool contiguous = true;
+		std::vector<uint64_t> dst_off(nb);
+		for (uint32_t i = 0; i < nb; ++i) {
+			if (st[i].code == DS_PRE_BLOCK_REF) {
+				pre = true;  // B.Indep set, but the block reads earlier blocks (D2)
+				continue;
+			}
+			if (st[i].code != DS_OK)
+				return BULK_EXACT;
+			if ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum)
+				return BULK_EXACT;
+			dst_off[i] = bt_total;
+			if (bt_total != d[i].out_off)
+				contiguous = false;
+			bt_total += st[i].out_len;
+		}
+		if (pre)
+			return BULK_PRE_REF;
+		const uint8_t* d_res = d_out.p;
+		if (!contiguous) {
+			DevBuf<uint64_t> d_off;
+			if (!try_reserve(d_compact, size_t(std::max<uint64_t>(bt_total, 1))))
+				return BULK_EXACT;
+			d_off.reserve(nb);
+			HIP_OK(hipMemcpy(d_off.p, dst_off.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice));
+			HIP_OK(launch_compact(d_out.p, d_desc.p, d_off.p, d_st.p, nb, d_compact.p, stream));
+			HIP_OK(hipDeviceSynchronize());
+			d_res = d_compact.p;
+		}
+		uint8_t* dst = out.room(int64_t(bt_total));
+		if (h)  // D2H overlapped with the host XXH32 chain (content_xxh32_d2h)
+			content_xxh32_d2h(*h, d_res, int64_t(bt_total), dst, stream);
+		else if (bt_total)
+			HIP_OK(hipMemcpy(dst, d_res, size_t(bt_total), hipMemcpyDeviceToHost));
+		out.commit(int64_t(bt_total));
+		total += bt_total;
+		lo = hi;
+	}
+	return BULK_OK;
+}
+
+// Where a linked batch's resolved bytes go: dst(n) returns the device
+// buffer for the batch's n bytes (nullptr: no room), done(p, n) runs once
+// they are there.
+struct LinkedSink {
+	std::function<uint8_t*(int64_t)> dst;
+	std::function<void(const uint8_t*, int64_t)> done;
+};
+
+static void d2h(void* dst, const void* src, size_t n, hipStream_t stream)
+{
+	HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, stream));
+	HIP_OK(hipStreamSynchronize(stream));
+}
+
+// Linked frames (and independent ones whose blocks read earlier blocks,
+// D2): every block at once with synthetic history, resolved on the GPU
+// (lz4ada_linked.hip), batch by batch with the previous batch's last
+// 64 KiB carried as real history.  BULK_EXACT: the frame needs the exact
+// path (a block error or checksum mismatch, quirk D1, a reference before
+// the frame start, no device memory).
+static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block_max,
+                              const std::vector<lz4ada_block_desc>& descs, LinkedSink& sink,
+                              uint64_t& total, hipStream_t stream)
+{
+	// a batch holds 3 decode buffers (slots + 64 KiB regions) and one 4-byte
+	// word per output byte: ~7x its slot bytes
+	uint64_t budget = uint64_t(env_bytes("LZ4ADA_LINKED_BATCH_BYTES", int64_t(1) << 30));
+	DevBuf<uint8_t> d_tail[2];
+	d_tail[0].reserve(size_t(HISTORY_SIZE));
+	d_tail[1].reserve(size_t(HISTORY_SIZE));
+	HIP_OK(hipMemsetAsync(d_tail[0].p, 0, size_t(HISTORY_SIZE), stream));
+	int cur = 0;
+	// the reference's Output_Pos / Output_Pos_History (lz4ada.adb:678-690,
+	// 785-787), for quirk D1
+	int64_t opos = 0, oph = 0;
+	uint32_t lo = 0;
+	total = 0;
+	while (lo < descs.size()) {
+		const auto bt = batches_of(std::vector<lz4ada_block_desc>(descs.begin() + lo, descs.end()),
+		                           block_max, uint64_t(HISTORY_SIZE), budget);
+		const uint32_t hi = lo + bt[0].second;
+		const uint32_t nb = hi - lo;
+		std::vector<lz4ada_block_desc> d(descs.begin() + lo, descs.begin() + hi);
+		uint64_t bytes = 0;
+		for (auto& x : d) {
+			x.out_cap = slot_cap(x, block_max);
+			x.out_off = bytes + uint64_t(HISTORY_SIZE);
+			bytes += uint64_t(HISTORY_SIZE) + round256(x.out_cap);
+		}
+		DevBuf<uint8_t> bx, by, bh, tab;
+		if (!try_reserve(bx, size_t(bytes)) || !try_reserve(by, size_t(bytes)) ||
+		    !try_reserve(bh, size_t(bytes)) ||
+		    !try_reserve(tab, index_table_bytes(frame_len, nb))) {
+			if (budget > (uint64_t(64) << 20) && nb > 1) {
+				budget /= 2;
+				continue;
+			}
+			return BULK_EXACT;
+		}
+		DevBuf<lz4ada_block_desc> d_desc;
+		DevBuf<lz4ada_block_status> sx, sy, sh;
+		d_desc.reserve(nb);
+		sx.reserve(nb);
+		sy.reserve(nb);
+		sh.reserve(nb);
+		const size_t sb = nb * sizeof(lz4ada_block_status);
+		HIP_OK(hipMemcpyAsync(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc),
+		                      hipMemcpyHostToDevice, stream));
+		HIP_OK(hipMemsetAsync(sx.p, 0, sb, stream));
+		HIP_OK(launch_link_fill(bx.p, by.p, bh.p, d_desc.p, nb, stream));
+		HIP_OK(launch_block_checksums(d_frame, d_desc.p, nb, sx.p, stream));
+		HIP_OK(launch_index(d_frame, frame_len, d_desc.p, nb, tab.p, sx.p, stream));
+		HIP_OK(hipMemcpyAsync(sy.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
+		HIP_OK(hipMemcpyAsync(sh.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
+		uint8_t* bufs[3] = { bx.p, by.p, bh.p };
+		lz4ada_block_status* sts[3] = { sx.p, sy.p, sh.p };
+		for (int k = 0; k < 3; ++k) {
+			HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bufs[k], sts[k], 2,
+			                             stream));
+			HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bufs[k], sts[k], 1, LINK_HIST,
+			                        stream));
+		}
+		std::vector<lz4ada_block_status> st(nb);
+		d2h(st.data(), sx.p, sb, stream);
+		std::vector<int64_t> A(nb);
+		int64_t n = 0;
+		for (uint32_t i = 0; i < nb; ++i) {
+			if (st[i].code != DS_OK)
+				return BULK_EXACT;
+			if ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum)
+				return BULK_EXACT;
+			// D1: a match reaching >= D1_OFF back into
+			// the history right after a block that ended at 65536..65542
+			if (opos >= HISTORY_SIZE)
+				opos = 0;
+			if ((st[i].aux & AUX_D1_RISK) && oph >= HISTORY_SIZE && oph <= HISTORY_SIZE + 6)
+				return BULK_EXACT;
+			opos += st[i].out_len;
+			if (opos >= HISTORY_SIZE)
+				oph = opos;
+			A[i] = n;
+			n += st[i].out_len;
+		}
+		if (n >= (int64_t(1) << 31) - HISTORY_SIZE) {  // words hold positions + 65536 in 31 bits
+			if (nb > 1) {
+				budget /= 2;
+				continue;
+			}
+			return BULK_EXACT;
+		}
+		DevBuf<int64_t> d_A;
+		DevBuf<uint32_t> d_P, d_ctr;
+		if (!try_reserve(d_P, size_t(std::max<int64_t>(n, 1))))
+			return BULK_EXACT;
+		d_A.reserve(nb);
+		d_ctr.reserve(2);
+		HIP_OK(hipMemcpyAsync(d_A.p, A.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+		HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
+		HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p,
+		                        d_ctr.p, stream));
+		uint32_t ctr[2] = { 0, 0 };
+		d2h(ctr, d_ctr.p, sizeof ctr, stream);
+		bx.release();
+		by.release();
+		bh.release();
+		const int64_t tail_valid = std::min<int64_t>(int64_t(total), HISTORY_SIZE);
+		for (int round = 0; ctr[0] > 0; ++round) {
+			if (round > 64)
+				return BULK_EXACT;  // never expected: every pointer goes strictly back
+			HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
+			HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, d_ctr.p, stream));
+			d2h(ctr, d_ctr.p, sizeof ctr, stream);
+			if (ctr[1])
+				return BULK_EXACT;  // a reference before the frame start: the exact error
+		}
+		uint8_t* F = sink.dst(n);
+		if (!F)
+			return BULK_EXACT;
+		HIP_OK(launch_link_emit(d_P.p, n, F, stream));
+		HIP_OK(launch_link_tail(F, n, d_tail[cur].p, d_tail[cur ^ 1].p, stream));
+		cur ^= 1;
+		sink.done(F, n);
+		total += uint64_t(n);
+		lo = hi;
+	}
+	return BULK_OK;
+}
+
+// Which paths the last lz4ada_decode_* call on this thread took
+// (LZ4ADA_PATH_* bits; tests and diagnostics).
+static thread_local int g_last_path = 0;
+
+// One frame from host memory (Single_Frame semantics): the bulk path when
+// the frame indexes cleanly, else -- or when the bulk path finds anything
+// the reference would report or treat differently -- the exact path, which
+// raises the reference's exception in the reference's order.
+static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& consumed)
 {
 	lz4ada_frame_info info;
 	std::vector<lz4ada_block_desc> descs;
@@ -1403,25 +1649,61 @@ static void decode_one_frame(const uint8_t* f, int64_t len, uint8_t* out, int64_
 		indexed = false;  // the exact path raises the reference's error in order
 	}
 	if (indexed && info.format == LZ4ADA_FORMAT_SKIPPABLE && info.frame_len <= len) {
-		out_len = 0;  // Skip (lz4ada.adb:420-433): nothing to decode
-		consumed = info.frame_len;
+		consumed = info.frame_len;  // Skip (lz4ada.adb:420-433): nothing to decode
 		return;
 	}
-	if (indexed && info.format == LZ4ADA_FORMAT_MODERN && info.frame_len <= len &&
-	    (info.independent ||
-	     (info.block_max >= (256 << 10) && !getenv("LZ4ADA_NO_FAST_LINKED")))) {
-		if (fast_frame(f, len, info, descs, out, out_cap, out_len, !info.independent)) {
-			consumed = info.frame_len;
-			return;
+	const int64_t base = out.len;
+	if (indexed && info.frame_len <= len && info.format != LZ4ADA_FORMAT_SKIPPABLE &&
+	    !getenv("LZ4ADA_EXACT_ONLY")) {
+		device_check_or_raise();
+		DevBuf<uint8_t> d_frame;
+		if (try_reserve(d_frame, size_t(info.frame_len))) {
+			HIP_OK(hipMemcpy(d_frame.p, f, size_t(info.frame_len), hipMemcpyHostToDevice));
+			lz4ada_xxh32_state hs;
+			lz4ada_xxh32_reset(&hs, 0);
+			lz4ada_xxh32_state* h = info.content_checksum ? &hs : nullptr;
+			uint64_t total = 0;
+			// the reference decodes every frame as linked (B.Indep is never
+			// read, lz4ada.adb:267-275); independent blocks are the fast case
+			BulkResult r = BULK_PRE_REF;
+			if (info.independent && !getenv("LZ4ADA_FORCE_LINKED"))
+				r = bulk_independent(d_frame.p, info, descs, out, h, total);
+			const bool linked = r == BULK_PRE_REF;
+			if (linked) {
+				out.len = base;
+				lz4ada_xxh32_reset(&hs, 0);
+				DevBuf<uint8_t> d_F;
+				LinkedSink ls;
+				ls.dst = [&](int64_t n) -> uint8_t* {
+					return try_reserve(d_F, size_t(std::max<int64_t>(n, 1))) ? d_F.p : nullptr;
+				};
+				ls.done = [&](const uint8_t* F, int64_t n) {
+					uint8_t* dst = out.room(n);
+					if (h)
+						content_xxh32_d2h(*h, F, n, dst, nullptr);
+					else if (n)
+						HIP_OK(hipMemcpy(dst, F, size_t(n), hipMemcpyDeviceToHost));
+					out.commit(n);
+				};
+				r = bulk_linked(d_frame.p, uint64_t(info.frame_len), info.block_max, descs, ls, total,
+				                nullptr);
+			}
+			if (r == BULK_OK && (!info.has_content_size || total == info.content_size) &&
+			    (!h || (total == 0 ? 0x02cc5d05u : hs.hash) == info.content_checksum_declared)) {
+				consumed = info.frame_len;
+				g_last_path |= linked ? LZ4ADA_PATH_LINKED : LZ4ADA_PATH_INDEPENDENT;
+				return;
+			}
+			out.len = base;
 		}
 	}
 	// A legacy frame has no end mark: it ends where the next magic starts
 	// (what tool_unlz4ada's per-frame re-init achieves), so hand the exact
 	// path only this frame's bytes.
 	const int64_t flen = (indexed && info.format == LZ4ADA_FORMAT_LEGACY) ? info.frame_len : len;
-	exact_frame(f, flen, out, out_cap, out_len, consumed);
+	g_last_path |= LZ4ADA_PATH_EXACT;
+	exact_frame(f, flen, out, consumed);
 }
-
 }  // namespace lz4ada
 
 extern "C" {
@@ -1508,30 +1790,127 @@ int lz4ada_output_checksums_device(const void* d_out, const lz4ada_block_desc* d
 	});
 }
 
+// A stream's next frame starts with fewer than 7 bytes left: what the
+// reference CLI raises there (tool_unlz4ada/unlz4ada.adb:65-76), before
+// Init_With_Header's precondition (lz4ada.ads:243) would.
+static void partial_frame_check(int64_t left)
+{
+	if (left < 7)
+		raise(LZ4ADA_CONSTRAINT_ERROR, "Partial frame detected. Unable to process all data");
+}
+
 int lz4ada_decode_frame(const uint8_t* frame, int64_t len, uint8_t* out, int64_t out_cap,
                         int64_t* out_len, int64_t* frame_consumed)
 {
 	*out_len = 0;
 	*frame_consumed = 0;
-	return guarded(nullptr, [&] { decode_one_frame(frame, len, out, out_cap, *out_len, *frame_consumed); });
+	g_last_path = 0;
+	return guarded(nullptr, [&] {
+		Sink s;
+		s.p = out;
+		s.cap = out_cap;
+		decode_one_frame(frame, len, s, *frame_consumed);
+		*out_len = s.len;
+	});
 }
 
 int lz4ada_decode_stream(const uint8_t* input, int64_t len, uint8_t* out, int64_t out_cap,
                          int64_t* out_len)
 {
 	*out_len = 0;
+	g_last_path = 0;
 	return guarded(nullptr, [&] {
+		Sink s;
+		s.p = out;
+		s.cap = out_cap;
 		int64_t pos = 0;
 		while (pos < len) {
-			int64_t n = 0, c = 0;
-			decode_one_frame(input + pos, len - pos, out + *out_len, out_cap - *out_len, n, c);
-			*out_len += n;
+			int64_t c = 0;
+			partial_frame_check(len - pos);
+			decode_one_frame(input + pos, len - pos, s, c);
+			*out_len = s.len;
 			if (c <= 0)
 				raise(LZ4ADA_CONSTRAINT_ERROR, "decoder made no progress");
 			pos += c;
 		}
 	});
 }
+
+// The same into a buffer the library allocates and grows (no bound needed
+// up front); release it with lz4ada_buffer_free.  On failure *out is NULL.
+static int decode_alloc(const uint8_t* input, int64_t len, bool stream, uint8_t** out,
+                        int64_t* out_len, int64_t* consumed)
+{
+	*out = nullptr;
+	*out_len = 0;
+	if (consumed)
+		*consumed = 0;
+	Sink s;
+	s.growable = true;
+	g_last_path = 0;
+	const int st = guarded(nullptr, [&] {
+		int64_t pos = 0;
+		do {
+			int64_t c = 0;
+			if (stream)
+				partial_frame_check(len - pos);
+			decode_one_frame(input + pos, len - pos, s, c);
+			if (c <= 0)
+				raise(LZ4ADA_CONSTRAINT_ERROR, "decoder made no progress");
+			pos += c;
+		} while (stream && pos < len);
+		if (consumed)
+			*consumed = pos;
+	});
+	if (st != LZ4ADA_OK) {
+		free(s.p);
+		return st;
+	}
+	*out = s.p ? s.p : static_cast<uint8_t*>(malloc(1));
+	*out_len = s.len;
+	return LZ4ADA_OK;
+}
+
+int lz4ada_decode_frame_alloc(const uint8_t* frame, int64_t len, uint8_t** out, int64_t* out_len,
+                              int64_t* frame_consumed)
+{
+	return decode_alloc(frame, len, false, out, out_len, frame_consumed);
+}
+
+int lz4ada_decode_stream_alloc(const uint8_t* input, int64_t len, uint8_t** out, int64_t* out_len)
+{
+	return decode_alloc(input, len, true, out, out_len, nullptr);
+}
+
+void lz4ada_buffer_free(uint8_t* p) { free(p); }
+
+int lz4ada_decode_linked_device(const void* d_frame, uint64_t frame_len,
+                                const lz4ada_block_desc* descs, int64_t nblocks, int64_t block_max,
+                                void* d_out, int64_t out_cap, int64_t* out_len, void* stream)
+{
+	*out_len = 0;
+	return guarded(nullptr, [&] {
+		device_check_or_raise();
+		std::vector<lz4ada_block_desc> v(descs, descs + nblocks);
+		hipStream_t s = static_cast<hipStream_t>(stream);
+		int64_t pos = 0;
+		LinkedSink ls;
+		ls.dst = [&](int64_t n) -> uint8_t* {
+			return pos + n <= out_cap ? static_cast<uint8_t*>(d_out) + pos : nullptr;
+		};
+		ls.done = [&](const uint8_t*, int64_t n) { pos += n; };
+		uint64_t total = 0;
+		if (bulk_linked(static_cast<const uint8_t*>(d_frame), frame_len, block_max, v, ls, total,
+		                s) != BULK_OK)
+			raise(LZ4ADA_EXACT_PATH,
+			      "the frame needs the reference-exact path (lz4ada_decode_frame): a block "
+			      "error or checksum mismatch, quirk D1, or too little output room");
+		HIP_OK(hipStreamSynchronize(s));
+		*out_len = pos;
+	});
+}
+
+int lz4ada_last_path(void) { return g_last_path; }
 
 int64_t lz4ada_decoded_bound(const uint8_t* input, int64_t len)
 {

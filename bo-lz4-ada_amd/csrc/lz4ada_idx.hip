@@ -312,10 +312,11 @@ struct alignas(16) IdxLds {
 // (ghi[2k]; long RLE runs).  used counts the sub-segments holding a start.
 __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t s, int32_t seg_end,
                                                 int32_t n, uint32_t* rb, uint16_t* rc, uint32_t* ghi,
-                                                int32_t& used, bool& err)
+                                                int32_t& used, bool& err, int32_t& epos)
 {
 	err = false;
 	used = 0;
+	epos = INT32_MAX;
 	auto put = [&](int32_t k, uint32_t b, uint32_t c) {
 		rb[k] = b;
 		rc[k] = uint16_t(min(c, 0xFFFFu));
@@ -342,6 +343,7 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 		Seq q;
 		if (!parse_fast(S, p, n, q)) {
 			err = true;
+			epos = p;
 			return seg_end;
 		}
 		cnt += uint32_t(q.L + q.ml);
@@ -439,9 +441,10 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 		// is crossed in one step instead of one iteration per segment.
 		int32_t ein = (lane == 0) ? E : s;
 		uint32_t* ghi = reinterpret_cast<uint32_t*>(tab + (C >> 5) + NSUB * lane) + 1;
-		int32_t used = 0;
+		int32_t used = 0, epos = INT32_MAX;
 		bool err = false;
-		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used, err)
+		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used,
+		                                   err, epos)
 		                    : ein;
 		ISTAMP(I_WALK0);
 		for (int it = 0; it < 64; ++it) {
@@ -455,7 +458,8 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			if (changed) {
 				ein = prev;
 				if (s < n) {
-					y = walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used, err);
+					y = walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used, err,
+					                 epos);
 				} else {
 					y = ein;
 					err = false;
@@ -948,6 +952,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 	ISTAMP_DECL;
 	int32_t o_batch = 0;  // output position of the current batch
 	bool bad = false;
+	bool d1 = false;  // a match with offset >= D1_OFF reads before the block start
 	for (int32_t k0 = 0; k0 < nsub && !bad;) {
 		// stage input so that [k0*SUB, k0*SUB + 4 KiB) is readable
 		const int32_t cf = (k0 * SUB + mis) / BATCH;
@@ -1065,6 +1070,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					if (rml[r] > 0) {
 						if (roff[r] > mdst + hb)
 							pre = true;  // reference before the block start (D2) / history
+						if (roff[r] > mdst && roff[r] >= D1_OFF)
+							d1 = true;
 						if (mdst - roff[r] < glo)
 							anyg = true;
 					}
@@ -1270,6 +1277,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		k0 += m;
 		ISTAMP(D_FLUSH);
 	}
+	d1 = __any(d1);
 	if (!bad && lane == 0 && (o_batch & 15))  // last partial unit
 		gstore_n(ob + (o_batch & ~15), *reinterpret_cast<const u32x4*>(&D.oring[(o_batch & ~15) & OMASK]),
 		         o_batch & 15);
@@ -1278,7 +1286,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			status[b].code = DS_RETRY;
 		} else {
 			status[b].code = DS_OK;
-			status[b].aux = 0;
+			status[b].aux = d1 ? AUX_D1_RISK : 0;
 			status[b].detail = 0;
 			status[b].err_out_pos = 0;
 			status[b].out_len = uint32_t(o_batch);
@@ -1289,11 +1297,13 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 	return bad ? DS_RETRY : DS_OK;
 }
 
-// Independent blocks: one wave per block.  Linked frames (linked != 0,
-// launched as one workgroup): the blocks in order, each reading the
-// previous ones' output as history while every block so far is full (its
-// slot then continues the previous one); a declined or short block leaves
-// every later block DS_RETRY for the exact path.  Pinned to two waves per
+// Independent blocks (linked 0): one wave per block.  Linked frames in the
+// history layout of lz4ada_linked.hip (linked 2): one wave per block, each
+// slot preceded by LINK_HIST readable bytes.  Linked frames in contiguous
+// slots (linked 1, launched as one workgroup): the blocks in order, each
+// reading the previous ones' output as history while every block so far is
+// full (its slot then continues the previous one); a declined or short
+// block leaves every later block DS_RETRY for the exact path.  Pinned to two waves per
 // SIMD (at most 256 registers, so the allocator never reaches for AGPRs):
 // LDS allows 8 waves per CU, and the bench's 2048 blocks are all resident.
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_idx(const uint8_t* __restrict__ frame,
@@ -1306,14 +1316,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 {
 	__shared__ DecLds D;
 	// one call site of decode_block for both modes (code size)
-	int64_t hist = 0;
-	uint32_t b = linked ? 0u : blockIdx.x;
-	const uint32_t bend = linked ? nblocks : min(blockIdx.x + 1u, nblocks);
+	int64_t hist = linked == 2 ? LINK_HIST : 0;
+	uint32_t b = linked == 1 ? 0u : blockIdx.x;
+	const uint32_t bend = linked == 1 ? nblocks : min(blockIdx.x + 1u, nblocks);
 	for (; b < bend; ++b) {
 		int32_t len;
 		const int32_t code = decode_block(D, frame, frame_len, desc, b, tab_all, out, status,
 		                                  hist, len);
-		if (!linked)
+		if (linked != 1)
 			return;
 		vm_wait();  // the next block reads this output as history
 		__syncthreads();
@@ -1326,7 +1336,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 		}
 		hist += len;
 	}
-	if (!linked)
+	if (linked != 1)
 		return;
 	for (uint32_t r = b + lane_id(); r < nblocks; r += 64)
 		if (status[r].code == DS_OK || r > b)
@@ -1350,25 +1360,51 @@ extern "C" int lz4ada_idx_stamps(unsigned long long* out, int reset)
 }
 #endif
 
+// index table: 8 records of 8 bytes per 256-byte segment, per block at
+// record ((in_off >> 8) + b) * 8
+size_t index_table_bytes(uint64_t frame_len, uint32_t nblocks)
+{
+	return ((size_t(frame_len) >> 8) + size_t(nblocks) + 2) * 64;
+}
+
+hipError_t launch_index(const uint8_t* d_frame, uint64_t frame_len, const lz4ada_block_desc* d_desc,
+                        uint32_t nblocks, uint8_t* d_tab, lz4ada_block_status* d_status,
+                        hipStream_t stream)
+{
+	if (nblocks == 0)
+		return hipSuccess;
+	hipLaunchKernelGGL(idx::k_index, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len, d_desc,
+	                   nblocks, d_tab, d_status);
+	return hipGetLastError();
+}
+
+hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                 const uint8_t* d_tab, uint8_t* d_out,
+                                 lz4ada_block_status* d_status, int mode, hipStream_t stream)
+{
+	if (nblocks == 0)
+		return hipSuccess;
+	hipLaunchKernelGGL(idx::k_decode_idx, dim3(mode == 1 ? 1 : nblocks), dim3(64), 0, stream, d_frame,
+	                   frame_len, d_desc, nblocks, d_tab, d_out, d_status, mode);
+	return hipGetLastError();
+}
+
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
                              const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
                              lz4ada_block_status* d_status, hipStream_t stream, int linked)
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	// index table: 8 records of 8 bytes per 256-byte segment, per block at
-	// record ((in_off >> 8) + b) * 8
-	const size_t tab_len = ((size_t(frame_len) >> 8) + size_t(nblocks) + 2) * 64;
 	void* tab = nullptr;
-	hipError_t err = hipMallocAsync(&tab, tab_len, stream);
+	hipError_t err = hipMallocAsync(&tab, index_table_bytes(frame_len, nblocks), stream);
 	if (err != hipSuccess)
 		return err;
-	hipLaunchKernelGGL(idx::k_index, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len, d_desc,
-	                   nblocks, static_cast<uint8_t*>(tab), d_status);
-	hipLaunchKernelGGL(idx::k_decode_idx, dim3(linked ? 1 : nblocks), dim3(64), 0, stream, d_frame,
-	                   frame_len, d_desc, nblocks, static_cast<const uint8_t*>(tab), d_out, d_status,
-	                   linked);
-	err = hipGetLastError();
+	err = launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab), d_status,
+	                   stream);
+	if (err == hipSuccess)
+		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
+		                            static_cast<const uint8_t*>(tab), d_out, d_status, linked, stream);
 	const hipError_t e2 = hipFreeAsync(tab, stream);
 	return err != hipSuccess ? err : e2;
 }

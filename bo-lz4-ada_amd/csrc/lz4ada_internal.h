@@ -19,6 +19,18 @@ constexpr uint32_t P5 = 374761393u;
 constexpr int64_t HISTORY_SIZE = 65536;  // lz4ada.ads:350
 constexpr int64_t BLOCK_SIZE_BYTES = 4;  // lz4ada.ads:351
 
+// Linked frames (lz4ada_linked.hip): every block slot is preceded by this
+// many readable history bytes (the largest LZ4 offset).
+constexpr int32_t LINK_HIST = 65535;
+// Quirk D1: the reference's 8-byte wild copy (lz4ada.adb:811-817) may
+// clobber history bytes [Output_Pos + 1, Output_Pos + 7] before a match
+// reads them; that needs Output_Pos_History in [65536, 65542] and an offset
+// >= Output_Pos_History - 7 >= D1_OFF.  The decoders flag every block with
+// such a match reaching before its start (status aux bit AUX_D1_RISK on a
+// DS_OK block) and the host sends those frames to the exact path.
+constexpr int32_t D1_OFF = int32_t(HISTORY_SIZE) - 7;
+constexpr int32_t AUX_D1_RISK = 1;
+
 // Device status codes written by the decode kernels (per block).
 enum DevStatus : int32_t {
 	DS_OK = 0,
@@ -82,6 +94,29 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
                              const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
                              lz4ada_block_status* d_status, hipStream_t stream, int linked = 0);
 
+// Two-wave decoder alone (k_decode_pc).  retry_only: only blocks whose
+// status is DS_RETRY.  hist: output bytes readable right before every slot
+// (0 independent; LINK_HIST in the linked-frame layout).
+hipError_t launch_decode_pc(const uint8_t* d_frame, uint64_t frame_len,
+                            const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
+                            lz4ada_block_status* d_status, int retry_only, int32_t hist,
+                            hipStream_t stream);
+
+// Pass 1 of the index-driven decoder alone: the sequence-index table of
+// every block (index_table_bytes() of device memory at d_tab); declined
+// blocks get status DS_RETRY.
+size_t index_table_bytes(uint64_t frame_len, uint32_t nblocks);
+hipError_t launch_index(const uint8_t* d_frame, uint64_t frame_len, const lz4ada_block_desc* d_desc,
+                        uint32_t nblocks, uint8_t* d_tab, lz4ada_block_status* d_status,
+                        hipStream_t stream);
+// Pass 2 over a table from launch_index.  mode 0: independent blocks; 1:
+// the serial linked decoder (one workgroup, blocks in order); 2: every
+// block at once with LINK_HIST readable history bytes before its slot.
+hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                 const uint8_t* d_tab, uint8_t* d_out,
+                                 lz4ada_block_status* d_status, int mode, hipStream_t stream);
+
 // Per-block XXH32 of the compressed payloads (block checksums).
 hipError_t launch_block_checksums(const uint8_t* d_frame,
                                   const lz4ada_block_desc* d_desc, uint32_t nblocks,
@@ -102,6 +137,20 @@ hipError_t launch_xxh32_update(lz4ada_xxh32_state* d_state, const uint8_t* d_dat
 hipError_t launch_serial_block(uint8_t* d_buf, int64_t buflen, const uint8_t* d_blk,
                                int64_t raw_len, int64_t data_len, int compressed,
                                SerialState* d_state, hipStream_t stream);
+
+// Linked frames, every block at once (lz4ada_linked.hip).  Slots of the
+// three decode buffers are preceded by 64 KiB history regions.
+hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_block_desc* d_desc,
+                            uint32_t nblocks, hipStream_t stream);
+hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
+                            const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
+                            const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
+                            uint32_t* d_ctr, hipStream_t stream);
+hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
+                            uint32_t* d_ctr, hipStream_t stream);
+hipError_t launch_link_emit(const uint32_t* d_P, int64_t n, uint8_t* d_F, hipStream_t stream);
+hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail_old,
+                            uint8_t* d_tail_new, hipStream_t stream);
 
 // Gather variable-length slots into a contiguous buffer (short blocks).
 hipError_t launch_compact(const uint8_t* d_src, const lz4ada_block_desc* d_desc,

@@ -385,8 +385,13 @@ __device__ __forceinline__ void wave_mem_fence()
 	asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
+// hist: output bytes readable right before the block's slot (0 for
+// independent blocks; 65535 in the linked-frame layout of lz4ada_linked.hip).
+// d1: set when a match with offset >= D1_OFF reads before the block start
+// (the only matches the reference's wild-copy overshoot can corrupt, D1).
 __device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
-                          int64_t cap, int64_t& s, int64_t& o, lz4ada_block_status& st)
+                          int64_t cap, int64_t& s, int64_t& o, lz4ada_block_status& st,
+                          int32_t hist, bool& d1)
 {
 	const uint32_t lane = lane_id();
 	int64_t p = s;
@@ -444,7 +449,9 @@ __device__ bool one_token(cg8* __restrict__ in, int64_t n, g8* __restrict__ ob,
 	}
 	const int64_t ml = M + 4;
 	const int64_t q0 = o - off;
-	if (q0 < 0) {
+	if (q0 < 0 && off >= D1_OFF)
+		d1 = true;
+	if (q0 < -int64_t(hist)) {
 		st.code = DS_PRE_BLOCK_REF;
 		st.detail = q0;
 		st.err_out_pos = o;
@@ -1077,7 +1084,8 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 			done = true;
 		} else if (stop) {
 			int64_t s64 = s, o64 = o;
-			if (!one_token(in, n, ob, cap, s64, o64, st)) {
+			bool d1_unused = false;
+			if (!one_token(in, n, ob, cap, s64, o64, st, 0, d1_unused)) {
 				ok = false;
 				done = true;
 			} else {
@@ -1246,14 +1254,15 @@ __device__ __forceinline__ uint32_t win_next(uint32_t t, uint32_t p)
 #define PC_LOAD16(dst, p) __builtin_memcpy((dst), (p), 16)
 #endif
 
-__device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* __restrict__ ob STAMP_PARAM)
+__device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* __restrict__ ob,
+                                              int32_t hist STAMP_PARAM)
 {
 	const int lane = int(lane_id());
 	const int32_t nb = L.m_nb[c], blen = L.m_blen[c], o = L.m_o[c];
 	uint8_t* const outb = L.outx + 16;
 	if (L.tail_end != o) {  // first batch, or output written by the one-token path
 		if (lane < 16)
-			L.outx[lane] = (o - 16 + lane >= 0) ? ob[o - 16 + lane] : 0;
+			L.outx[lane] = (o - 16 + lane >= -hist) ? ob[o - 16 + lane] : 0;
 		if (lane == 0)
 			L.tail_end = o;
 		wave_mem_fence();
@@ -1405,7 +1414,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
                                                     const lz4ada_block_desc* __restrict__ desc,
                                                     uint32_t nblocks, uint8_t* __restrict__ out,
                                                     lz4ada_block_status* __restrict__ status,
-                                                    int retry_only)
+                                                    int retry_only, int32_t hist)
 {
 	__shared__ PcLds L;
 
@@ -1458,6 +1467,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 		pf1 = load_chunk(in, lim_addr, hi + 1024);
 	}
 	bool ok = true;
+	bool d1 = false;  // a match with offset >= D1_OFF reads before the block start
 	bool pdone = (n == 0);
 	bool smode = false;  // sequences are long: parse them one at a time
 	if (threadIdx.x < PC_SLOTS)
@@ -1527,8 +1537,9 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 						const int32_t klen = t.L + t.ml;
 						const int32_t d0 = o + blen + t.L;
 						okp = okp && nb < MAXTOK && klen <= PC_BIG && blen + klen <= OUTB &&
-						      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
+						      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= -hist) &&
 						      (t.off >= 16 || t.ml <= 64);
+						d1 = d1 || (okp && t.kind == TK_NORMAL && d0 < t.off && t.off >= D1_OFF);
 						if (!okp) {
 							if (nb == 0)
 								stop = true;
@@ -1649,10 +1660,11 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 					const int32_t d0 = o + tstart + kL;
 					const bool fits = good && lane < MAXTOK - nb && klen <= PC_BIG &&
 					                  blen + incl <= OUTB && o + blen + incl <= cap &&
-					                  (kkind != TK_NORMAL || d0 - koff >= 0) &&
+					                  (kkind != TK_NORMAL || d0 - koff >= -hist) &&
 					                  (koff >= 16 || kml <= 64);
 					const uint64_t badm = __ballot(!fits);
 					const int cnt = badm ? (__ffsll((long long)badm) - 1) : 64;
+					d1 = d1 || (lane < cnt && kkind == TK_NORMAL && d0 < koff && koff >= D1_OFF);
 					const int32_t cnext = cnt > 0 ? __shfl(knext, cnt - 1) : s;
 					const int32_t ckind_last = cnt > 0 ? __shfl(kkind, cnt - 1) : TK_NORMAL;
 					if (lane < cnt) {
@@ -1713,7 +1725,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 						__builtin_amdgcn_s_sleep(1);
 				STAMP(SP_WAIT);
 				int64_t s64 = s, o64 = o;
-				if (!one_token(in, n, ob, cap, s64, o64, st)) {
+				if (!one_token(in, n, ob, cap, s64, o64, st, hist, d1)) {
 					ok = false;
 					pdone = true;
 				} else {
@@ -1726,6 +1738,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 				STAMP(SP_ONE);
 			}
 		}
+		d1 = __any(d1);
 		wave_lds_fence();
 		if (lane == 0)
 			L.pdone = 1;
@@ -1745,7 +1758,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 			if (!have)
 				break;
 			asm volatile("" ::: "memory");
-			pc_copy_batch(L, cs, mis, ob STAMP_ARGS);
+			pc_copy_batch(L, cs, mis, ob, hist STAMP_ARGS);
 			wave_lds_fence();
 			if (lane == 0)
 				L.full[cs] = 0;
@@ -1756,7 +1769,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 
 	if (threadIdx.x == 0) {
 		status[b].code = ok ? int32_t(DS_OK) : st.code;
-		status[b].aux = st.aux;
+		status[b].aux = ok ? (d1 ? AUX_D1_RISK : 0) : st.aux;
 		status[b].detail = st.detail;
 		status[b].err_out_pos = st.err_out_pos;
 		status[b].out_len = uint32_t(o);
@@ -2009,7 +2022,7 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 		return hipSuccess;
 	if (variant == DEC_PC) {
 		hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
-		                   d_desc, nblocks, d_out, d_status, 0);
+		                   d_desc, nblocks, d_out, d_status, 0, 0);
 		return hipGetLastError();
 	}
 	if (variant == DEC_IDX_LINKED)
@@ -2020,7 +2033,7 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 		if (err != hipSuccess || variant == DEC_IDX_ALONE)
 			return err;
 		hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
-		                   d_desc, nblocks, d_out, d_status, 1);
+		                   d_desc, nblocks, d_out, d_status, 1, 0);
 		return hipGetLastError();
 	}
 	if (variant == DEC_WG) {
@@ -2031,6 +2044,18 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 	}
 	hipLaunchKernelGGL(k_decode_blocks, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
 	                   d_desc, nblocks, d_out, d_status, variant == DEC_WG ? 1 : 0);
+	return hipGetLastError();
+}
+
+hipError_t launch_decode_pc(const uint8_t* d_frame, uint64_t frame_len,
+                            const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
+                            lz4ada_block_status* d_status, int retry_only, int32_t hist,
+                            hipStream_t stream)
+{
+	if (nblocks == 0)
+		return hipSuccess;
+	hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len, d_desc,
+	                   nblocks, d_out, d_status, retry_only, hist);
 	return hipGetLastError();
 }
 

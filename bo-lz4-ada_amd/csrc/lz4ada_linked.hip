@@ -1,0 +1,272 @@
+// lz4ada_linked.hip -- every block of a LINKED frame at once (SURVEY §8f
+// item 3).  gfx950 / MI355X.
+//
+// In a linked frame a block's matches may read up to 65535 bytes of the
+// output before it (lz4ada.adb:845-904 with the Output_Pos_History scheme
+// of :678-690, 785-787).  That makes the blocks one serial chain if they are
+// decoded with real history.  Here each block is decoded with a SYNTHETIC
+// history instead, so every block runs at once:
+//
+//  * layout: every block's output slot is preceded by a 64 KiB history
+//    region (desc.out_off - 65536), so the decoders read "before the block
+//    start" like any other output byte (k_decode_idx mode 2, k_decode_pc
+//    with hist = LINK_HIST);
+//  * three decodes of the whole batch with different history patterns at
+//    position k of the region: X = k & 255, Y = ~X, H = k >> 8.  Decoding
+//    only moves bytes, so an output byte equal in X and Y is a constant (a
+//    literal, maybe copied on), and one that differs came from history
+//    position k = X | H << 8 -- byte (k - 65536) relative to its block start;
+//  * k_link_init turns the three outputs into one word per output byte, a
+//    resolved byte or a pointer to an earlier position of the frame;
+//  * k_link_jump resolves the pointers by pointer jumping (each round
+//    replaces a pointer by its target's word, so chains through many
+//    blocks finish in ~log2(length) rounds), reading positions before the
+//    batch from the previous batch's last 64 KiB;
+//  * k_link_emit writes the bytes.
+//
+// The result equals decoding the frame with contiguous history.  The
+// reference differs from that only in quirk D1 (wild-copy overshoot into
+// history), which the host detects from the decoders' AUX_D1_RISK flags and
+// the Output_Pos_History sequence, and in references before the frame
+// start, which k_link_jump reports; both send the frame to the exact path.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "lz4ada_internal.h"
+#include "lz4ada_dev.h"
+
+namespace lz4ada {
+
+namespace link {
+
+constexpr uint32_t RES = 0x80000000u;  // resolved: low byte is the value
+constexpr int TPB = 256;
+
+// Wave sum -> one global atomic per wave (vector atomic, not scalar).
+__device__ __forceinline__ void wave_count(uint32_t* ctr, uint32_t v)
+{
+#pragma unroll
+	for (int o = 32; o >= 1; o >>= 1)
+		v += __shfl_xor(v, o);
+	if (lane_id() == 0 && v)
+		atomicAdd(ctr, v);
+}
+
+// History regions of the three decode buffers.
+__global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint8_t* __restrict__ y,
+                                                   uint8_t* __restrict__ h,
+                                                   const lz4ada_block_desc* __restrict__ desc,
+                                                   uint32_t nblocks)
+{
+	const uint32_t b = blockIdx.x;
+	if (b >= nblocks)
+		return;
+	const uint64_t base = desc[b].out_off - uint64_t(HISTORY_SIZE);
+	for (uint32_t c = blockIdx.y * TPB + threadIdx.x; c < HISTORY_SIZE / 16; c += gridDim.y * TPB) {
+		const uint32_t k0 = 16u * c;
+		u32x4 vx;
+		uint32_t w[4];
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			const uint32_t k = (k0 + 4u * i) & 255u;
+			w[i] = k | ((k + 1u) << 8) | ((k + 2u) << 16) | ((k + 3u) << 24);
+		}
+		vx = u32x4{ w[0], w[1], w[2], w[3] };
+		const uint32_t hi = (k0 >> 8) * 0x01010101u;
+		*reinterpret_cast<GLOBAL u32x4*>(gptr(x) + base + k0) = vx;
+		*reinterpret_cast<GLOBAL u32x4*>(gptr(y) + base + k0) = ~vx;
+		*reinterpret_cast<GLOBAL u32x4*>(gptr(h) + base + k0) = u32x4{ hi, hi, hi, hi };
+	}
+}
+
+// One word per output byte of the batch (batch-relative position a =
+// A[b] + q): RES | byte, or the encoded position of the byte it copies,
+// (source position) + 65536 -- always >= 0, and below a.
+__global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x,
+                                                   const uint8_t* __restrict__ y,
+                                                   const uint8_t* __restrict__ h,
+                                                   const lz4ada_block_desc* __restrict__ desc,
+                                                   const lz4ada_block_status* __restrict__ st,
+                                                   const int64_t* __restrict__ A, uint32_t nblocks,
+                                                   uint32_t* __restrict__ P,
+                                                   uint32_t* __restrict__ ctr)
+{
+	const uint32_t b = blockIdx.x;
+	if (b >= nblocks)
+		return;
+	const uint64_t ob = desc[b].out_off;
+	const int64_t len = st[b].out_len;
+	const int64_t ab = A[b];
+	uint32_t unres = 0;
+	for (int64_t q0 = 16 * (int64_t(blockIdx.y) * TPB + threadIdx.x); q0 < len;
+	     q0 += 16 * int64_t(gridDim.y) * TPB) {
+		const u32x4 vx = *reinterpret_cast<const GLOBAL u32x4*>(gptr(x) + ob + q0);
+		const u32x4 vy = *reinterpret_cast<const GLOBAL u32x4*>(gptr(y) + ob + q0);
+		const u32x4 vh = *reinterpret_cast<const GLOBAL u32x4*>(gptr(h) + ob + q0);
+		const uint32_t wx[4] = { vx.x, vx.y, vx.z, vx.w };
+		const uint32_t wy[4] = { vy.x, vy.y, vy.z, vy.w };
+		const uint32_t wh[4] = { vh.x, vh.y, vh.z, vh.w };
+		GLOBAL uint32_t* dst = gptr(P) + ab + q0;
+		const int32_t m = int32_t(len - q0 < 16 ? len - q0 : 16);
+#pragma unroll
+		for (int i = 0; i < 16; ++i) {
+			if (i < m) {
+				const uint32_t bx = (wx[i >> 2] >> (8 * (i & 3))) & 255u;
+				const uint32_t by = (wy[i >> 2] >> (8 * (i & 3))) & 255u;
+				const uint32_t bh = (wh[i >> 2] >> (8 * (i & 3))) & 255u;
+				uint32_t v;
+				if (bx == by) {
+					v = RES | bx;
+				} else {
+					// history position k = bx | bh << 8 is byte k - 65536 of
+					// the block-relative output: source ab + k - 65536
+					v = uint32_t(ab + int64_t(bx | (bh << 8)));
+					++unres;
+				}
+				dst[i] = v;
+			}
+		}
+	}
+	wave_count(ctr, unres);
+}
+
+// One pointer-jumping round over P[0, n).  ctr[0]: words still unresolved
+// after the round; ctr[1]: references before the frame start (positions
+// below -tail_valid).  tail: the 65536 output bytes before the batch.
+__global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int64_t n,
+                                                   const uint8_t* __restrict__ tail,
+                                                   int64_t tail_valid, uint32_t* __restrict__ ctr)
+{
+	uint32_t unres = 0, bad = 0;
+	GLOBAL uint32_t* Pg = gptr(P);
+	for (int64_t a0 = 4 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
+	     a0 += 4 * int64_t(gridDim.x) * TPB) {
+		uint32_t w[4];
+		if (a0 + 4 <= n) {
+			const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(Pg + a0);
+			w[0] = v.x;
+			w[1] = v.y;
+			w[2] = v.z;
+			w[3] = v.w;
+		} else {
+#pragma unroll
+			for (int i = 0; i < 4; ++i)
+				w[i] = a0 + i < n ? Pg[a0 + i] : RES;
+		}
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			if (w[i] & RES)
+				continue;
+			const int64_t t = int64_t(w[i]) - HISTORY_SIZE;
+			uint32_t f;
+			if (t >= 0) {
+				f = Pg[t];  // the source's word: resolved, or a pointer further back
+			} else if (t >= -tail_valid) {
+				f = RES | tail[HISTORY_SIZE + t];
+			} else {
+				++bad;
+				continue;
+			}
+			Pg[a0 + i] = f;
+			if (!(f & RES))
+				++unres;
+		}
+	}
+	wave_count(&ctr[0], unres);
+	wave_count(&ctr[1], bad);
+}
+
+// Bytes of the resolved words.
+__global__ __launch_bounds__(TPB) void k_link_emit(const uint32_t* __restrict__ P, int64_t n,
+                                                   uint8_t* __restrict__ F)
+{
+	for (int64_t a0 = 16 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
+	     a0 += 16 * int64_t(gridDim.x) * TPB) {
+		if (a0 + 16 <= n) {
+			uint32_t o[4];
+#pragma unroll
+			for (int j = 0; j < 4; ++j) {
+				const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(gptr(P) + a0 + 4 * j);
+				o[j] = (v.x & 255u) | ((v.y & 255u) << 8) | ((v.z & 255u) << 16) | ((v.w & 255u) << 24);
+			}
+			*reinterpret_cast<GLOBAL u32x4*>(gptr(F) + a0) = u32x4{ o[0], o[1], o[2], o[3] };
+		} else {
+			for (int64_t a = a0; a < n; ++a)
+				F[a] = uint8_t(P[a]);
+		}
+	}
+}
+
+// tail_new = the last 65536 bytes of (tail_old ++ F[0, n)).
+__global__ __launch_bounds__(TPB) void k_link_tail(const uint8_t* __restrict__ F, int64_t n,
+                                                   const uint8_t* __restrict__ tail_old,
+                                                   uint8_t* __restrict__ tail_new)
+{
+	for (int64_t i = int64_t(blockIdx.x) * TPB + threadIdx.x; i < HISTORY_SIZE;
+	     i += int64_t(gridDim.x) * TPB) {
+		const int64_t p = n - HISTORY_SIZE + i;
+		tail_new[i] = p >= 0 ? F[p] : tail_old[HISTORY_SIZE + p];
+	}
+}
+
+}  // namespace link
+
+hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_block_desc* d_desc,
+                            uint32_t nblocks, hipStream_t stream)
+{
+	if (nblocks == 0)
+		return hipSuccess;
+	hipLaunchKernelGGL(link::k_link_fill, dim3(nblocks, 4), dim3(link::TPB), 0, stream, x, y, h, d_desc,
+	                   nblocks);
+	return hipGetLastError();
+}
+
+hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
+                            const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
+                            const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
+                            uint32_t* d_ctr, hipStream_t stream)
+{
+	if (nblocks == 0)
+		return hipSuccess;
+	const int64_t per = 16 * link::TPB;
+	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
+	hipLaunchKernelGGL(link::k_link_init, dim3(nblocks, gy), dim3(link::TPB), 0, stream, x, y, h, d_desc,
+	                   d_st, d_A, nblocks, d_P, d_ctr);
+	return hipGetLastError();
+}
+
+static uint32_t grid_for(int64_t n, int64_t per_thread)
+{
+	const int64_t per = per_thread * link::TPB;
+	return uint32_t(std::min<int64_t>(8192, std::max<int64_t>(1, (n + per - 1) / per)));
+}
+
+hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
+                            uint32_t* d_ctr, hipStream_t stream)
+{
+	if (n <= 0)
+		return hipSuccess;
+	hipLaunchKernelGGL(link::k_link_jump, dim3(grid_for(n, 4)), dim3(link::TPB), 0, stream, d_P, n, d_tail,
+	                   tail_valid, d_ctr);
+	return hipGetLastError();
+}
+
+hipError_t launch_link_emit(const uint32_t* d_P, int64_t n, uint8_t* d_F, hipStream_t stream)
+{
+	if (n <= 0)
+		return hipSuccess;
+	hipLaunchKernelGGL(link::k_link_emit, dim3(grid_for(n, 16)), dim3(link::TPB), 0, stream, d_P, n, d_F);
+	return hipGetLastError();
+}
+
+hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail_old, uint8_t* d_tail_new,
+                            hipStream_t stream)
+{
+	hipLaunchKernelGGL(link::k_link_tail, dim3(64), dim3(link::TPB), 0, stream, d_F, n, d_tail_old,
+	                   d_tail_new);
+	return hipGetLastError();
+}
+
+}  // namespace lz4ada

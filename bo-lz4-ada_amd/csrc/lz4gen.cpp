@@ -3,7 +3,7 @@
 // model, together with their decoded bytes, so that benches and GPU tests
 // need no external compressor on the GPU box.  Block rules honoured: the
 // last sequence is literal-only with >= 12 literals when the block allows,
-// offsets lie in [1, min(pos, 65535)].
+// offsets lie in [1, min(pos, 65535)].  kind 4 (chain) is for linked frames.
 #include <stdint.h>
 #include <string.h>
 
@@ -94,6 +94,12 @@ static int64_t gen_block(int kind, uint64_t seed, uint8_t* raw, int64_t raw_len,
 			L = pos == 0 ? 1 : 0;
 			ml = 4 + r.geo(60000.0);
 			break;
+		case 4:  // chain: matches only (short offsets), so in a linked frame
+		         // every byte copies the previous block's tail -- pointer
+		         // chains through every block (lz4ada_linked.hip worst case)
+			L = 0;
+			ml = 4 + r.geo(100.0);
+			break;
 		default:  // literal-heavy
 			L = 64 + r.geo(400.0);
 			ml = 4 + r.geo(3.0);
@@ -119,6 +125,8 @@ static int64_t gen_block(int kind, uint64_t seed, uint8_t* raw, int64_t raw_len,
 			const int64_t maxoff = pos + hist < 65535 ? pos + hist : 65535;
 			if (kind == 2)
 				off = 1;
+			else if (kind == 4)
+				off = 1 + r.below(uint32_t(maxoff < 16 ? maxoff : 16));
 			else if (kind == 1 && r.below(4) == 0)
 				off = 1 + r.below(uint32_t(maxoff < 64 ? maxoff : 64));
 			else

@@ -111,8 +111,15 @@ class DeviceError(LZ4AdaError):
     ada_name = "LZ4ADA.DEVICE_ERROR"
 
 
+class NeedsExactPath(LZ4AdaError):
+    """A device-only call declined the frame: lz4ada.decode_frame gives the
+    reference's result (output or exception)."""
+    ada_name = "LZ4ADA.EXACT_PATH"
+
+
 _ERRORS = {1: ChecksumError, 2: DataCorruption, 3: NotSupported, 4: TooFewHeaderBytes,
-           5: TooLittleMemory, 6: AssertionFailure, 7: ConstraintError, 8: DeviceError}
+           5: TooLittleMemory, 6: AssertionFailure, 7: ConstraintError, 8: DeviceError,
+           9: NeedsExactPath}
 
 
 def _check(status: int, message: str):
@@ -191,6 +198,12 @@ _sig = {
     "lz4ada_output_checksums_device": ([_vp, _vp, _vp, _i64, _vp, _vp], ctypes.c_int),
     "lz4ada_decode_frame": ([_vp, _i64, _vp, _i64, _pi64, _pi64], ctypes.c_int),
     "lz4ada_decode_stream": ([_vp, _i64, _vp, _i64, _pi64], ctypes.c_int),
+    "lz4ada_decode_frame_alloc": ([_vp, _i64, _P(_vp), _pi64, _pi64], ctypes.c_int),
+    "lz4ada_decode_stream_alloc": ([_vp, _i64, _P(_vp), _pi64], ctypes.c_int),
+    "lz4ada_buffer_free": ([_vp], None),
+    "lz4ada_last_path": ([], ctypes.c_int),
+    "lz4ada_decode_linked_device": ([_vp, ctypes.c_uint64, _vp, _i64, _i64, _vp, _i64, _pi64, _vp],
+                                    ctypes.c_int),
     "lz4ada_decoded_bound": ([_vp, _i64], _i64),
     "lz4ada_gen_block": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _vp, _i64], _i64),
     "lz4ada_gen_block_linked": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _i64, _vp, _i64], _i64),
@@ -351,27 +364,41 @@ def decoded_bound(data) -> int:
     return _lib.lz4ada_decoded_bound(_addr(data), len(data))
 
 
+def _take(p, n: int) -> bytes:
+    """Copy out and release a buffer from a lz4ada_decode_*_alloc call."""
+    try:
+        return ctypes.string_at(p, n) if n else b""
+    finally:
+        _lib.lz4ada_buffer_free(p)
+
+
 def decode_frame(data, offset: int = 0):
-    """One frame (Single_Frame semantics) -> (decoded bytes, bytes consumed)."""
+    """One frame (Single_Frame semantics) -> (decoded bytes, bytes consumed).
+    The library sizes the output itself, so any frame -- also one whose
+    later bytes do not index -- raises the reference's own exception."""
     n = len(data) - offset
-    bound = _lib.lz4ada_decoded_bound(_addr(data, offset), n)
-    cap = max(bound, 0) + (64 << 10)
-    out = ctypes.create_string_buffer(max(cap, 1))
-    olen, cons = _i64(), _i64()
-    _check(_lib.lz4ada_decode_frame(_addr(data, offset), n, out, cap, ctypes.byref(olen),
-                                    ctypes.byref(cons)), _thread_error())
-    return out.raw[:olen.value], cons.value
+    p, olen, cons = _vp(), _i64(), _i64()
+    _check(_lib.lz4ada_decode_frame_alloc(_addr(data, offset), n, ctypes.byref(p),
+                                          ctypes.byref(olen), ctypes.byref(cons)),
+           _thread_error())
+    return _take(p, olen.value), cons.value
 
 
 def decode_stream(data) -> bytes:
     """Every frame of a concatenated stream -> decoded bytes."""
-    bound = _lib.lz4ada_decoded_bound(_addr(data), len(data))
-    cap = max(bound, 0) + (64 << 10)
-    out = ctypes.create_string_buffer(max(cap, 1))
-    olen = _i64()
-    _check(_lib.lz4ada_decode_stream(_addr(data), len(data), out, cap, ctypes.byref(olen)),
-           _thread_error())
-    return out.raw[:olen.value]
+    p, olen = _vp(), _i64()
+    _check(_lib.lz4ada_decode_stream_alloc(_addr(data), len(data), ctypes.byref(p),
+                                           ctypes.byref(olen)), _thread_error())
+    return _take(p, olen.value)
+
+
+PATH_INDEPENDENT, PATH_LINKED, PATH_EXACT = 1, 2, 4
+
+
+def last_path() -> int:
+    """PATH_* bits of the paths the last decode_frame / decode_stream call on
+    this thread took (bulk independent, bulk linked, reference-exact)."""
+    return _lib.lz4ada_last_path()
 
 
 def decode_blocks_device(d_frame: int, frame_len: int, d_descs: int, nblocks: int, d_out: int,
@@ -379,6 +406,17 @@ def decode_blocks_device(d_frame: int, frame_len: int, d_descs: int, nblocks: in
     """Launch block checksums + decode over device-resident buffers (async)."""
     _check(_lib.lz4ada_decode_blocks_device(d_frame, frame_len, d_descs, nblocks, d_out,
                                             d_status, stream), _thread_error())
+
+
+def decode_linked_device(d_frame: int, frame_len: int, descs, nblocks: int, block_max: int,
+                         d_out: int, out_cap: int, stream: int = 0) -> int:
+    """Linked-frame bulk path over a device-resident frame (host descriptors
+    from frame_index) into contiguous device output -> decoded length.
+    Raises NeedsExactPath when decode_frame must give the reference's result."""
+    olen = _i64()
+    _check(_lib.lz4ada_decode_linked_device(d_frame, frame_len, descs, nblocks, block_max, d_out,
+                                            out_cap, ctypes.byref(olen), stream), _thread_error())
+    return olen.value
 
 
 def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=0):
@@ -418,8 +456,9 @@ def output_checksums_device(d_out, d_descs, d_status, nblocks, d_hash, stream=0)
 
 # ---------------------------------------------------------- synthetic data
 
-GEN_DENSE, GEN_MIXED, GEN_RLE, GEN_LITERAL = 0, 1, 2, 3
-GEN_KINDS = {"dense": GEN_DENSE, "mixed": GEN_MIXED, "rle": GEN_RLE, "literal": GEN_LITERAL}
+GEN_DENSE, GEN_MIXED, GEN_RLE, GEN_LITERAL, GEN_CHAIN = 0, 1, 2, 3, 4
+GEN_KINDS = {"dense": GEN_DENSE, "mixed": GEN_MIXED, "rle": GEN_RLE, "literal": GEN_LITERAL,
+             "chain": GEN_CHAIN}
 
 
 def gen_block(kind: int, seed: int, raw_len: int):
@@ -433,12 +472,17 @@ def gen_block(kind: int, seed: int, raw_len: int):
     return comp.raw[:n], raw.raw[:raw_len]
 
 
-def gen_linked_blocks(kind: int, seed: int, block_len: int, nblocks: int, last_len=None):
+def gen_linked_blocks(kind: int, seed: int, block_len: int, nblocks: int, last_len=None,
+                      lens=None):
     """Blocks of one linked frame whose matches reach back into the earlier
-    blocks' output (up to 64 KiB) -> list of (payload, decoded)."""
+    blocks' output (up to 64 KiB) -> list of (payload, decoded).  lens: the
+    decoded length of every block (overrides block_len / nblocks / last_len)."""
+    if lens is None:
+        lens = [block_len] * nblocks
+        if last_len is not None and nblocks:
+            lens[-1] = last_len
     out, hist = [], b""
-    for i in range(nblocks):
-        raw_len = last_len if (last_len is not None and i == nblocks - 1) else block_len
+    for i, raw_len in enumerate(lens):
         h = hist[-65536:]
         buf = ctypes.create_string_buffer(h + bytes(max(raw_len, 1)), len(h) + max(raw_len, 1))
         cap = raw_len + raw_len // 128 + 64 + raw_len // 200 + 1024

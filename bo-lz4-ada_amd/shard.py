@@ -1,20 +1,29 @@
 """Multi-GPU sharding of independent-block frames.
 
-One process per GPU (torch.distributed, RCCL over xGMI for the one
-collective).  A frame whose blocks are independent (FLG.B.Indep) is split
+One process per GPU (torch.distributed, RCCL over xGMI for the few small
+collectives).  A frame whose blocks are independent (FLG.B.Indep) is split
 into contiguous block ranges, balanced by compressed bytes; each rank copies
 only its range of the compressed frame to its GPU and decodes it with
-``lz4ada_decode_blocks_device`` — no data-path collective.  The ranks agree
-on one error status with a single ``all_reduce(MAX)``; on any error every
-rank re-runs the frame through the exact single-GPU path
+``lz4ada_decode_blocks_device`` -- no data-path collective.  Then:
+
+* the ranks agree on one block status with a single ``all_reduce(MAX)``;
+* the frame-level checks of ``Check_End_Mark`` (lz4ada.adb:463-523) run
+  across ranks: the declared content size against the ``all_reduce(SUM)``
+  of the decoded lengths, and the content checksum as ONE XXH32 chain in
+  frame order -- rank r receives the running 48-byte hasher state from
+  rank r-1, hashes its own decoded bytes (D2H + host chain,
+  ``lz4ada_content_xxh32_d2h``), and passes it on; the last rank's Final
+  value is broadcast.  The chain is serial by nature.
+
+On any failure every rank re-runs the frame through the single-GPU path
 (``lz4ada.decode_frame``) so it raises the reference's exception and message
-(lz4ada.adb:661-707 error precedence) — the same decision on every rank.
+-- the same decision on every rank.
 
 Linked frames (B.Indep = 0) do not shard: they decode on one GPU
 ("replicas only").
 """
 import ctypes
-from typing import List, Sequence, Tuple
+from typing import Callable, List, Sequence, Tuple
 
 import lz4ada  # noqa: F401  (imports torch first: one HIP runtime)
 import torch
@@ -87,22 +96,124 @@ def block_errors(descs, statuses) -> List[int]:
     return bad
 
 
+def _dist_on() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def reduce_status(local: int, group=None, device=None) -> int:
-    """The one collective: MAX of the per-rank status."""
-    if not dist.is_available() or not dist.is_initialized():
+    """The one status collective: MAX of the per-rank status."""
+    if not _dist_on():
         return local
     t = torch.tensor([local], dtype=torch.int32, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return int(t.item())
 
 
-def decode_frame_sharded(frame: bytes, rank: int, world: int, device, group=None):
+def reduce_sum(local: int, group=None, device=None) -> int:
+    """SUM over ranks (decoded bytes, for the declared content size)."""
+    if not _dist_on():
+        return local
+    t = torch.tensor([local], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return int(t.item())
+
+
+def _global(group, r: int) -> int:
+    return dist.get_global_rank(group, r) if group is not None else r
+
+
+XXH32_EMPTY = 0x02CC5D05  # XXH32 of no bytes, seed 0 (vector `empty`, SURVEY App. B)
+
+
+def chain_xxh32(init: bytes, update_local: Callable[[bytes], bytes],
+                finalize: Callable[[bytes], int], rank: int, world: int, group=None,
+                device=None) -> int:
+    """ONE XXH32 chain over every rank's bytes in rank order (a frame-wide
+    content checksum, lz4ada.adb:709-714, 493-501).  The hasher state is an
+    opaque byte string: rank 0 starts from `init`, every rank applies
+    `update_local` to the state it receives from rank-1 and sends the result
+    to rank+1; the last rank's `finalize` value is broadcast to all."""
+    if world > 1 and not _dist_on():
+        raise ValueError("a content checksum across ranks needs an initialised process group")
+    state = init
+    if rank > 0:
+        t = torch.empty(len(init), dtype=torch.uint8, device=device)
+        dist.recv(t, src=_global(group, rank - 1), group=group)
+        state = bytes(t.cpu().numpy().tobytes())
+    state = update_local(state)
+    if rank + 1 < world:
+        t = torch.frombuffer(bytearray(state), dtype=torch.uint8).to(device)
+        dist.send(t, dst=_global(group, rank + 1), group=group)
+    h = finalize(state) if rank == world - 1 else 0
+    if world > 1:
+        t = torch.tensor([h], dtype=torch.int64, device=device)
+        dist.broadcast(t, src=_global(group, world - 1), group=group)
+        h = int(t.item())
+    return h
+
+
+def _device_runs(local, k: int, out_lens: Sequence[int]):
+    """(offset, length) runs of consecutive decoded bytes in a rank's slots."""
+    runs = []
+    for j in range(k):
+        off, n = local[j].out_off, int(out_lens[j])
+        if runs and runs[-1][0] + runs[-1][1] == off:
+            runs[-1] = (runs[-1][0], runs[-1][1] + n)
+        elif n:
+            runs.append((off, n))
+    return runs
+
+
+def _product_hasher(d_out, runs, stream: int):
+    """update_local / finalize over the product's hasher state: the rank's
+    decoded bytes stream to the host chain (lz4ada_content_xxh32_d2h)."""
+    size = ctypes.sizeof(lz4ada.XXH32State)
+
+    def update(state: bytes) -> bytes:
+        st = lz4ada.XXH32State.from_buffer_copy(state)
+        for off, n in runs:
+            lz4ada._check(lz4ada._lib.lz4ada_content_xxh32_d2h(
+                ctypes.byref(st), d_out.data_ptr() + off, n, None, stream), lz4ada._thread_error())
+        return bytes(st)[:size]
+
+    def final(state: bytes) -> int:
+        st = lz4ada.XXH32State.from_buffer_copy(state)
+        return st.hash if st.total_length else XXH32_EMPTY
+
+    init = lz4ada.XXH32State()
+    lz4ada._lib.lz4ada_xxh32_reset(ctypes.byref(init), 0)
+    return bytes(init)[:size], update, final
+
+
+def frame_checks_ok(info, total_local: int, hasher, rank: int, world: int, group=None,
+                    device=None) -> bool:
+    """Check_End_Mark's frame-level checks across ranks (lz4ada.adb:463-523):
+    declared content size vs the summed decoded bytes, and the content
+    checksum chained in frame order.  Same answer on every rank."""
+    if world > 1 and not _dist_on() and (info.has_content_size or info.content_checksum):
+        raise ValueError("frame-level checks across ranks need an initialised process group")
+    total = reduce_sum(total_local, group, device)
+    if info.has_content_size and total != info.content_size:
+        return False
+    if info.content_checksum:
+        init, update, final = hasher()
+        if chain_xxh32(init, update, final, rank, world, group, device) != \
+                info.content_checksum_declared:
+            return False
+    return True
+
+
+def decode_frame_sharded(frame: bytes, rank: int, world: int, device, group=None,
+                         coll_device=None):
     """Decode this rank's share of an independent-block frame on `device`.
 
     Returns (d_out uint8 tensor, (lo, hi) block range, out_lens list).  The
     output stays resident on the rank's GPU (slots of block_max bytes).
-    Raises the reference exception (via the exact path) if any rank found
-    a bad block; linked frames raise ValueError (they do not shard)."""
+    Raises the reference exception (via the exact path) if any rank found a
+    bad block or the frame-level checks fail; linked frames raise ValueError
+    (they do not shard).  coll_device: device of the collectives' tensors
+    (default `device`; "cpu" for a gloo group)."""
+    coll = coll_device if coll_device is not None else device
     info, descs = lz4ada.frame_index(frame)
     if info.format != lz4ada.FORMAT_MODERN or not info.independent:
         raise ValueError("only independent-block modern frames shard")
@@ -113,13 +224,13 @@ def decode_frame_sharded(frame: bytes, rank: int, world: int, device, group=None
     d_out = torch.empty(max(out_bytes, 1), dtype=torch.uint8, device=device)
     status = SHARD_OK
     out_lens: List[int] = []
+    stream = torch.cuda.current_stream(device)
     if k:
         d_in = torch.frombuffer(bytearray(frame[b0:b1]), dtype=torch.uint8).to(device)
         d_desc = torch.frombuffer(bytearray(bytes(local)[:k * ctypes.sizeof(lz4ada.BlockDesc)]),
                                   dtype=torch.uint8).to(device)
         d_st = torch.zeros(k * ctypes.sizeof(lz4ada.BlockStatus), dtype=torch.uint8,
                            device=device)
-        stream = torch.cuda.current_stream(device)
         lz4ada.decode_blocks_device(d_in.data_ptr(), b1 - b0, d_desc.data_ptr(), k,
                                     d_out.data_ptr(), d_st.data_ptr(), stream.cuda_stream)
         stream.synchronize()
@@ -128,10 +239,17 @@ def decode_frame_sharded(frame: bytes, rank: int, world: int, device, group=None
         if block_errors([local[j] for j in range(k)], sts):
             status = SHARD_BLOCK_ERROR
         out_lens = [s.out_len for s in sts]
-    if reduce_status(status, group, device) != SHARD_OK:
+    ok = reduce_status(status, group, coll) == SHARD_OK
+    if ok:
+        runs = _device_runs(local, k, out_lens)
+        ok = frame_checks_ok(info, sum(out_lens),
+                             lambda: _product_hasher(d_out, runs, stream.cuda_stream),
+                             rank, world, group, coll)
+    if not ok:
         lz4ada.decode_frame(frame)  # raises the reference exception
-        # the exact path accepted it: a block reaches before its own start
-        # (B.Indep set but ignored by the reference) -> linked data
+        # the single-GPU path accepted it: a block reaches before its own
+        # start (B.Indep set but ignored by the reference) ->
+        # linked data, decoded by the linked path
         raise ValueError("frame has cross-block references (D2); decode it on one GPU "
                          "with lz4ada.decode_frame")
     return d_out, (lo, hi), out_lens

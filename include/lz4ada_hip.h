@@ -41,7 +41,8 @@ typedef enum {
 	LZ4ADA_TOO_LITTLE_MEMORY = 5,    /* LZ4Ada.Too_Little_Memory */
 	LZ4ADA_ASSERTION_ERROR = 6,      /* Pre/Assert violated (API misuse) */
 	LZ4ADA_CONSTRAINT_ERROR = 7,     /* library-internal check */
-	LZ4ADA_DEVICE_ERROR = 8          /* HIP error / no GPU (no reference twin) */
+	LZ4ADA_DEVICE_ERROR = 8,         /* HIP error / no GPU (no reference twin) */
+	LZ4ADA_EXACT_PATH = 9            /* device-only call: the frame needs lz4ada_decode_frame */
 } lz4ada_status;
 
 /* Flexible_Memory_Reservation (lz4ada.ads:79-106), same order. */
@@ -148,10 +149,13 @@ int lz4ada_xxh32_hash(const uint8_t *data, int64_t len, uint32_t *out);
  * decoded by its own wavefront on the GPU, with block checksums
  * (lz4ada.adb:698-707) verified on the GPU.  Output lands in per-block
  * slots of block_max bytes (desc.out_off), contiguous whenever every
- * non-last block is full.  A non-zero block status, a failed checksum, a
- * back-reference before its block start (linked / B.Indep=0 data) or an
- * oversize block sends lz4ada_decode_frame() down the reference-exact
- * serial path, which reproduces the reference's output and exception.
+ * non-last block is full.  lz4ada_decode_frame() decodes independent
+ * blocks this way; linked frames (and independent ones whose blocks read
+ * earlier blocks, quirk D2) decode every block at once against a synthetic
+ * history that the GPU then resolves.  A non-zero
+ * block status, a failed checksum, quirk D1 or a reference before the frame
+ * start sends the frame down the reference-exact serial path, which
+ * reproduces the reference's output and exception.
  */
 
 typedef struct {
@@ -261,7 +265,38 @@ int lz4ada_decode_frame(const uint8_t *frame, int64_t len, uint8_t *out, int64_t
 int lz4ada_decode_stream(const uint8_t *input, int64_t len, uint8_t *out, int64_t out_cap,
                          int64_t *out_len);
 
-/* Upper bound of the decoded size of a stream (sum of block maxima). */
+/* The same two calls into a buffer the library allocates and grows, so no
+ * bound is needed up front (a stream that fails to index part-way still
+ * raises the reference's own exception); release it with
+ * lz4ada_buffer_free().  On failure *out is NULL. */
+int lz4ada_decode_frame_alloc(const uint8_t *frame, int64_t len, uint8_t **out, int64_t *out_len,
+                              int64_t *frame_consumed);
+int lz4ada_decode_stream_alloc(const uint8_t *input, int64_t len, uint8_t **out,
+                               int64_t *out_len);
+void lz4ada_buffer_free(uint8_t *p);
+
+/* The linked-frame bulk path over a device-resident frame (BASELINE
+ * configs[4]): every block at once against a synthetic history, resolved
+ * on the GPU, into contiguous device output d_out
+ * (out_cap bytes); descs are the HOST descriptors from lz4ada_frame_index.
+ * Synchronous on `stream`.  Returns LZ4ADA_EXACT_PATH when the reference
+ * would raise or diverge (block error, checksum mismatch, quirk D1, a
+ * reference before the frame start) -- lz4ada_decode_frame() then gives
+ * the reference's result.  The content checksum is the caller's. */
+int lz4ada_decode_linked_device(const void *d_frame, uint64_t frame_len,
+                                const lz4ada_block_desc *descs, int64_t nblocks, int64_t block_max,
+                                void *d_out, int64_t out_cap, int64_t *out_len, void *stream);
+
+/* Paths the last lz4ada_decode_* call on this thread took (bit mask):
+ * independent blocks in bulk, linked blocks in bulk (synthetic history
+ * resolved on the GPU), the reference-exact serial path. */
+#define LZ4ADA_PATH_INDEPENDENT 1
+#define LZ4ADA_PATH_LINKED 2
+#define LZ4ADA_PATH_EXACT 4
+int lz4ada_last_path(void);
+
+/* Upper bound of the decoded size of a stream (sum of block maxima); -1 if
+ * some frame does not index (then use the _alloc calls). */
 int64_t lz4ada_decoded_bound(const uint8_t *input, int64_t len);
 
 /* ------------------------------------------------------------------ misc */

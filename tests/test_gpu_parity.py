@@ -507,9 +507,10 @@ def test_linked_frame_short_block_falls_back():
 
 
 @pytest.mark.gpu
-def test_linked_frame_64k_uses_exact_path():
-    """64 KiB linked blocks stay on the exact path (the reference's D1
-    overshoot corner case lives there); output equals the oracle's."""
+def test_linked_frame_64k():
+    """64 KiB linked blocks (the LZ4F default): the bulk linked path, or the
+    exact path where the reference's D1 overshoot could matter; output
+    equals the oracle's either way (tests/test_gpu_linked.py checks which)."""
     blocks = lz4ada.gen_linked_blocks(1, 11, 64 << 10, 4)
     frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], 64 << 10,
                                       indep=False)

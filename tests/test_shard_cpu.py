@@ -125,3 +125,78 @@ def test_linked_frames_do_not_shard():
     frame, _ = lz4frame.build_frame(blocks, 64 * KiB, indep=False)
     with pytest.raises(ValueError):
         shard.decode_frame_sharded(frame, 0, 1, torch.device("cpu"))
+
+
+# ---------------------------------------------- frame-level checks across ranks
+
+class _Info:
+    def __init__(self, has_size=False, size=0, cksum=False, declared=0):
+        self.has_content_size, self.content_size = has_size, size
+        self.content_checksum, self.content_checksum_declared = cksum, declared
+
+
+def _oracle_hasher(piece):
+    """update_local / finalize over the oracle's 48-byte hasher state (the
+    checker standing in for the product's D2H + host chain)."""
+    L = O.lib()
+
+    def make():
+        init = ctypes.create_string_buffer(48)
+        L.oracle_xxh32_reset(init, 0)
+
+        def update(state):
+            buf = ctypes.create_string_buffer(state, 48)
+            L.oracle_xxh32_update(buf, piece, len(piece))
+            return buf.raw
+
+        def final(state):
+            return L.oracle_xxh32_final(ctypes.create_string_buffer(state, 48))
+        return init.raw, update, final
+    return make
+
+
+def _checks_worker(rank, world, port, pieces, infos, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        piece = pieces[rank]
+        init, update, final = _oracle_hasher(piece)()
+        h = shard.chain_xxh32(init, update, final, rank, world, device="cpu")
+        oks = [shard.frame_checks_ok(_Info(*i), len(piece), _oracle_hasher(piece), rank, world,
+                                     device="cpu") for i in infos]
+        result_q.put((rank, h, oks))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_content_checksum_chains_across_ranks(world):
+    """chain_xxh32 = XXH32 of the concatenation in rank order, on every rank
+    (empty shares included), and frame_checks_ok agrees with the declared
+    content size / checksum exactly as Check_End_Mark would."""
+    import random
+    import xxhash
+    rng = random.Random(world)
+    sizes = [rng.randint(0, 70000) for _ in range(world)]
+    if world > 1:
+        sizes[1] = 0  # a rank with no blocks passes the state on unchanged
+    pieces = [rng.randbytes(n) for n in sizes]
+    whole = b"".join(pieces)
+    want = xxhash.xxh32(whole).intdigest()
+    infos = [(False, 0, False, 0), (True, len(whole), True, want), (True, len(whole) + 1, False, 0),
+             (False, 0, True, want ^ 1), (True, len(whole), False, 0)]
+    expect = [True, True, False, False, True]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_checks_worker, args=(world, free_port(), pieces, infos, q), nprocs=world,
+                       join=True, start_method="spawn")
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    for rank, h, oks in res:
+        assert h == want, rank
+        assert oks == expect, rank
+
+
+def test_empty_frame_chain_hash():
+    init, update, final = _oracle_hasher(b"")()
+    assert shard.chain_xxh32(init, update, final, 0, 1) == shard.XXH32_EMPTY
