@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -1350,6 +1351,34 @@ static bool try_reserve(DevBuf<T>& b, size_t count)
 	return true;
 }
 
+// Device scratch of the bulk path, kept per thread between calls: the
+// large buffers (slots, decode copies, resolution words) cost a hipMalloc
+// and a first-touch each time otherwise -- more than the decode itself on a
+// 1 GiB linked frame.  lz4ada_release_device_cache() frees them.  The
+// cache is never destroyed at thread exit (the HIP runtime may be gone).
+enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_TAB, SC_P, SC_F, SC_N };
+struct ScratchCache {
+	DevBuf<uint8_t> b[SC_N];
+};
+static ScratchCache& scratch_cache()
+{
+	static thread_local ScratchCache* c = new ScratchCache;
+	return *c;
+}
+static void scratch_release()
+{
+	for (auto& x : scratch_cache().b)
+		x.release();
+}
+// bytes of scratch `role`, or nullptr when the device has no room (the
+// caller then shrinks its batch or takes the exact path; other roles may be
+// in use, so they are kept)
+static uint8_t* scratch(int role, size_t bytes)
+{
+	DevBuf<uint8_t>& d = scratch_cache().b[role];
+	return try_reserve(d, bytes) ? d.p : nullptr;
+}
+
 static int64_t env_bytes(const char* name, int64_t dflt)
 {
 	const char* e = getenv(name);
@@ -1420,10 +1449,10 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 			x.out_off = slots;
 			slots += round256(x.out_cap);
 		}
-		DevBuf<uint8_t> d_out, d_compact;
 		DevBuf<lz4ada_block_desc> d_desc;
 		DevBuf<lz4ada_block_status> d_st;
-		if (!try_reserve(d_out, size_t(slots))) {
+		uint8_t* const d_out = scratch(SC_OUT, size_t(slots));
+		if (!d_out) {
 			if (budget > (uint64_t(64) << 20) && nb > 1) {
 				budget /= 2;  // retry this batch smaller
 				continue;
@@ -1435,7 +1464,7 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 		HIP_OK(hipMemcpy(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc), hipMemcpyHostToDevice));
 		HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
 		HIP_OK(launch_block_checksums(d_frame, d_desc.p, nb, d_st.p, stream));
-		HIP_OK(launch_decode_blocks(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out.p, d_st.p,
+		HIP_OK(launch_decode_blocks(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out, d_st.p,
 		                            stream));
 		std::vector<lz4ada_block_status> st(nb);
 		HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status), hipMemcpyDeviceToHost));
@@ -1459,16 +1488,17 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 		}
 		if (pre)
 			return BULK_PRE_REF;
-		const uint8_t* d_res = d_out.p;
+		const uint8_t* d_res = d_out;
 		if (!contiguous) {
 			DevBuf<uint64_t> d_off;
-			if (!try_reserve(d_compact, size_t(std::max<uint64_t>(bt_total, 1))))
+			uint8_t* const d_compact = scratch(SC_COMPACT, size_t(std::max<uint64_t>(bt_total, 1)));
+			if (!d_compact)
 				return BULK_EXACT;
 			d_off.reserve(nb);
 			HIP_OK(hipMemcpy(d_off.p, dst_off.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice));
-			HIP_OK(launch_compact(d_out.p, d_desc.p, d_off.p, d_st.p, nb, d_compact.p, stream));
+			HIP_OK(launch_compact(d_out, d_desc.p, d_off.p, d_st.p, nb, d_compact, stream));
 			HIP_OK(hipDeviceSynchronize());
-			d_res = d_compact.p;
+			d_res = d_compact;
 		}
 		uint8_t* dst = out.room(int64_t(bt_total));
 		if (h)  // D2H overlapped with the host XXH32 chain (content_xxh32_d2h)
@@ -1508,7 +1538,19 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 {
 	// a batch holds 3 decode buffers (slots + 64 KiB regions) and one 4-byte
 	// word per output byte: ~7x its slot bytes
-	uint64_t budget = uint64_t(env_bytes("LZ4ADA_LINKED_BATCH_BYTES", int64_t(1) << 30));
+	uint64_t budget = uint64_t(env_bytes("LZ4ADA_LINKED_BATCH_BYTES", int64_t(2) << 30));
+	// LZ4ADA_TRACE_LINKED=1: phase times (synchronised) to stderr
+	static const bool trace = getenv("LZ4ADA_TRACE_LINKED") != nullptr;
+	auto t0 = std::chrono::steady_clock::now();
+	auto phase = [&](const char* name) {
+		if (!trace)
+			return;
+		HIP_OK(hipStreamSynchronize(stream));
+		const auto t1 = std::chrono::steady_clock::now();
+		fprintf(stderr, "[linked] %-10s %8.3f ms\n", name,
+		        std::chrono::duration<double, std::milli>(t1 - t0).count());
+		t0 = t1;
+	};
 	DevBuf<uint8_t> d_tail[2];
 	d_tail[0].reserve(size_t(HISTORY_SIZE));
 	d_tail[1].reserve(size_t(HISTORY_SIZE));
@@ -1531,10 +1573,12 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			x.out_off = bytes + uint64_t(HISTORY_SIZE);
 			bytes += uint64_t(HISTORY_SIZE) + round256(x.out_cap);
 		}
-		DevBuf<uint8_t> bx, by, bh, tab;
-		if (!try_reserve(bx, size_t(bytes)) || !try_reserve(by, size_t(bytes)) ||
-		    !try_reserve(bh, size_t(bytes)) ||
-		    !try_reserve(tab, index_table_bytes(frame_len, nb))) {
+		struct {
+			uint8_t* p;
+		} bx{ scratch(SC_X, size_t(bytes)) }, by{ bx.p ? scratch(SC_Y, size_t(bytes)) : nullptr },
+		    bh{ by.p ? scratch(SC_H, size_t(bytes)) : nullptr },
+		    tab{ bh.p ? scratch(SC_TAB, index_table_bytes(frame_len, nb)) : nullptr };
+		if (!tab.p) {
 			if (budget > (uint64_t(64) << 20) && nb > 1) {
 				budget /= 2;
 				continue;
@@ -1548,6 +1592,7 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		sy.reserve(nb);
 		sh.reserve(nb);
 		const size_t sb = nb * sizeof(lz4ada_block_status);
+		phase("alloc");
 		HIP_OK(hipMemcpyAsync(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc),
 		                      hipMemcpyHostToDevice, stream));
 		HIP_OK(hipMemsetAsync(sx.p, 0, sb, stream));
@@ -1564,6 +1609,7 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bufs[k], sts[k], 1, LINK_HIST,
 			                        stream));
 		}
+		phase("decodes");
 		std::vector<lz4ada_block_status> st(nb);
 		d2h(st.data(), sx.p, sb, stream);
 		std::vector<int64_t> A(nb);
@@ -1593,8 +1639,11 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			return BULK_EXACT;
 		}
 		DevBuf<int64_t> d_A;
-		DevBuf<uint32_t> d_P, d_ctr;
-		if (!try_reserve(d_P, size_t(std::max<int64_t>(n, 1))))
+		DevBuf<uint32_t> d_ctr;
+		struct {
+			uint32_t* p;
+		} d_P{ reinterpret_cast<uint32_t*>(scratch(SC_P, size_t(std::max<int64_t>(n, 1)) * 4)) };
+		if (!d_P.p)
 			return BULK_EXACT;
 		d_A.reserve(nb);
 		d_ctr.reserve(2);
@@ -1604,9 +1653,7 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		                        d_ctr.p, stream));
 		uint32_t ctr[2] = { 0, 0 };
 		d2h(ctr, d_ctr.p, sizeof ctr, stream);
-		bx.release();
-		by.release();
-		bh.release();
+		phase("init");
 		const int64_t tail_valid = std::min<int64_t>(int64_t(total), HISTORY_SIZE);
 		for (int round = 0; ctr[0] > 0; ++round) {
 			if (round > 64)
@@ -1620,10 +1667,13 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		uint8_t* F = sink.dst(n);
 		if (!F)
 			return BULK_EXACT;
+		phase("jumps");
 		HIP_OK(launch_link_emit(d_P.p, n, F, stream));
 		HIP_OK(launch_link_tail(F, n, d_tail[cur].p, d_tail[cur ^ 1].p, stream));
 		cur ^= 1;
+		phase("emit");
 		sink.done(F, n);
+		phase("sink");
 		total += uint64_t(n);
 		lo = hi;
 	}
@@ -1656,8 +1706,10 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 	if (indexed && info.frame_len <= len && info.format != LZ4ADA_FORMAT_SKIPPABLE &&
 	    !getenv("LZ4ADA_EXACT_ONLY")) {
 		device_check_or_raise();
-		DevBuf<uint8_t> d_frame;
-		if (try_reserve(d_frame, size_t(info.frame_len))) {
+		struct {
+			uint8_t* p;
+		} d_frame{ scratch(SC_FRAME, size_t(info.frame_len)) };
+		if (d_frame.p) {
 			HIP_OK(hipMemcpy(d_frame.p, f, size_t(info.frame_len), hipMemcpyHostToDevice));
 			lz4ada_xxh32_state hs;
 			lz4ada_xxh32_reset(&hs, 0);
@@ -1672,10 +1724,9 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 			if (linked) {
 				out.len = base;
 				lz4ada_xxh32_reset(&hs, 0);
-				DevBuf<uint8_t> d_F;
 				LinkedSink ls;
 				ls.dst = [&](int64_t n) -> uint8_t* {
-					return try_reserve(d_F, size_t(std::max<int64_t>(n, 1))) ? d_F.p : nullptr;
+					return scratch(SC_F, size_t(std::max<int64_t>(n, 1)));
 				};
 				ls.done = [&](const uint8_t* F, int64_t n) {
 					uint8_t* dst = out.room(n);
@@ -1911,6 +1962,8 @@ int lz4ada_decode_linked_device(const void* d_frame, uint64_t frame_len,
 }
 
 int lz4ada_last_path(void) { return g_last_path; }
+
+void lz4ada_release_device_cache(void) { scratch_release(); }
 
 int64_t lz4ada_decoded_bound(const uint8_t* input, int64_t len)
 {

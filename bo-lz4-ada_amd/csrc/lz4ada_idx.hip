@@ -845,6 +845,152 @@ __device__ __forceinline__ void ring_match(DecLds& L, int32_t dst, int32_t off, 
 	}
 }
 
+// q = t / d and r = t mod d for 0 <= t < 2^22, 1 <= d < 2^16: float
+// reciprocal (error < 1 in q) and one correction step.
+__device__ __forceinline__ int32_t div_small(int32_t t, int32_t d, int32_t& r)
+{
+	int32_t q = int32_t(float(t) * __builtin_amdgcn_rcpf(float(d)));
+	r = t - q * d;
+	if (r < 0) {
+		--q;
+		r += d;
+	}
+	if (r >= d) {
+		++q;
+		r -= d;
+	}
+	return q;
+}
+
+// Store step of a period-off pattern match (make_pattern16's stp).
+__device__ __forceinline__ int32_t pattern_step(int32_t off)
+{
+	return off <= 8 ? int32_t((PAT_LUT >> (5 * (off - 1))) & 31u) : off;
+}
+
+__device__ __forceinline__ int32_t piece_owner(int32_t inc, int32_t t);
+
+// Every lane's match (dst, off, ml; ml = 0: none) with a source in the LDS
+// ring, cut into pieces dealt over the wave: 16 output bytes each, or stp
+// bytes of a period-off pattern (off < 16 < ml would overlap: match byte i
+// is source byte i mod off, so a piece never reads its own match's output).
+// Pieces are in output order; one reading output of a lower lane of its
+// chunk waits until that lane has stored (ballot per step).
+__device__ __forceinline__ void ring_pieces(DecLds& D, int32_t mdst, int32_t off, int32_t ml)
+{
+	const int32_t lane = int32_t(lane_id());
+	const bool pat = off < 16 && off < ml;
+	const int32_t stp = pat ? pattern_step(off) : 16;
+	int32_t rr;
+	const int32_t np = ml <= 0 ? 0 : (stp == 16 ? (ml + 15) >> 4 : div_small(ml + stp - 1, stp, rr));
+	const int32_t inc = wave_incl_scan(np);
+	const int32_t tot = __shfl(inc, 63);
+	for (int32_t t0 = 0; t0 < tot; t0 += 64) {
+		const int32_t t = t0 + lane;
+		const bool act = t < tot;
+		const int32_t lo = piece_owner(inc, act ? t : tot - 1);
+		const int32_t k = t - (__shfl(inc, lo) - __shfl(np, lo));
+		const int32_t od = __shfl(mdst, lo), ooff = __shfl(off, lo), oml = __shfl(ml, lo);
+		const int32_t ostp = __shfl(stp, lo);
+		const bool opat = ooff < 16 && ooff < oml;
+		const bool wide = !opat && oml > ooff;  // overlap with off >= 16
+		const int32_t pd = od + k * ostp;
+		const int32_t pn = min(16, oml - k * ostp);
+		// source bytes read: the whole period for patterns and overlaps
+		const int32_t s_lo = (opat || wide) ? od - ooff : od - ooff + 16 * k;
+		const int32_t s_hi = (opat || wide) ? od : s_lo + pn;
+		// lanes of this chunk whose piece [pd, pd + 16) meets [s_lo, s_hi):
+		// pd is monotone over the lanes, so two binary searches
+		const int32_t pe = act ? pd + 16 : INT32_MAX, ps = act ? pd : INT32_MAX;
+		int32_t j1 = 0, c2 = 0;
+#pragma unroll
+		for (int st = 32; st >= 1; st >>= 1) {
+			if (__shfl(pe, j1 + st - 1) <= s_lo)
+				j1 += st;
+			if (__shfl(ps, c2 + st - 1) < s_hi)
+				c2 += st;
+		}
+		const int32_t j2 = min(c2 - 1, lane - 1);
+		uint64_t dep = 0;
+		if (act && j1 <= j2)
+			dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
+		bool pend = act;
+		for (;;) {
+			const uint64_t pm = __ballot(pend);
+			if (pm == 0)
+				break;
+			const bool ready = pend && (dep & pm) == 0;
+			if (ready) {
+				u32x4 v;
+				if (opat) {
+					v = oload16(D, od - ooff);
+					int32_t sstp;
+					make_pattern16(uint64_t(v.x) | (uint64_t(v.y) << 32),
+					               uint64_t(v.z) | (uint64_t(v.w) << 32), ooff, v, sstp);
+				} else if (wide) {
+					int32_t rem;
+					div_small(16 * k, ooff, rem);
+					v = oload16(D, od - ooff + rem);
+					if (ooff - rem < 16)
+						v = merge_at(v, oload16(D, od - ooff + rem - ooff), ooff - rem);
+				} else {
+					v = oload16(D, s_lo);
+				}
+				ostore(D, pd, v, pn);
+			}
+			pend = pend && !ready;
+			wave_lds_fence();
+		}
+	}
+}
+
+// Ring-sourced matches of a round of short matches, one lane each: those
+// whose source is final before the round (or lies in their own literals)
+// at once, a near match -- reading this round's match output -- once every
+// lane whose output it reads is done (a 64-bit mask from two binary
+// searches over the round's monotone match positions, one AND against a
+// ballot per step).  rbeg: the round's first output position; L: this
+// lane's literal length.
+constexpr int RING_LANE_MAX = 32;
+__device__ __forceinline__ void ring_lanes(DecLds& D, int32_t mdst, int32_t off, int32_t ml,
+                                           int32_t rbeg, int32_t L)
+{
+	const int32_t lane = int32_t(lane_id());
+	const int32_t src = mdst - off;
+	const int32_t dep_end = src + min(off, ml);
+	const bool far = ml > 0 && (dep_end <= rbeg || off <= L);
+	bool near = ml > 0 && !far;
+	if (far)
+		ring_match(D, mdst, off, ml);
+	wave_lds_fence();
+	if (!__any(near))
+		return;
+	const int32_t mend = mdst + ml;
+	int32_t j1 = 0, c2 = 0;
+#pragma unroll
+	for (int st = 32; st >= 1; st >>= 1) {
+		if (__shfl(mend, j1 + st - 1) <= src)
+			j1 += st;
+		if (__shfl(mdst, c2 + st - 1) < dep_end)
+			c2 += st;
+	}
+	const int32_t j2 = min(c2 - 1, lane - 1);
+	uint64_t dep = 0;
+	if (near && j1 <= j2)
+		dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
+	for (;;) {
+		const uint64_t pending = __ballot(near);
+		if (pending == 0)
+			break;
+		const bool ready = near && (dep & pending) == 0;
+		if (ready) {
+			ring_match(D, mdst, off, ml);
+			near = false;
+		}
+		wave_lds_fence();
+	}
+}
+
 // Owner of piece t when lane i holds pieces [inc_i - cnt_i, inc_i) (inc: the
 // wave's inclusive prefix sum of piece counts): the first lane with inc > t.
 __device__ __forceinline__ int32_t piece_owner(int32_t inc, int32_t t)
@@ -1170,6 +1316,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		wave_lds_fence();
 		ISTAMP(D_LIT);
 
+#ifdef LZ4ADA_IDX_OLD_M
 		// M: matches, round by round in output order.  Everything before the
 		// round is final, so a match whose (non-self) source ends there (or
 		// lies in its own literals) runs at once; a near match -- one reading
@@ -1258,6 +1405,62 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				}
 			}
 		}
+#else
+		// M: matches, round by round in output order.  HBM-sourced matches
+		// store the pieces loaded in P.  Every match whose source is in the
+		// LDS ring -- before the round, in its own literals, or in this
+		// round's output (near) -- is cut into pieces dealt over the wave,
+		// 16 bytes each (a period-off pattern: stp bytes, so every piece
+		// starts at phase 0), so a round costs its piece count / 64, not
+		// its longest match.  A piece reading this chunk's output runs once
+		// every lower lane it reads from has stored (one AND against a
+		// ballot per step; pieces of one match never read each other: match
+		// byte i is source byte i mod off).
+#pragma unroll
+		for (int r = 0; r < RMAX; ++r) {
+			if (64 * r < N) {
+				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
+				const bool hbm = ml > 0 && mdst - off < glo;
+				if (hbm) {
+#pragma unroll
+					for (int c = 0; c < GC; ++c)
+						if (16 * c < ml)
+							ostore(D, mdst + 16 * c, vg[r][c], min(16, ml - 16 * c));
+				}
+				// pieces of HBM-sourced matches beyond the first GC: the first
+				// 64 of the round were loaded in P, dealt over the wave
+				if (rpn[r] > 0)
+					ostore(D, rpd[r], vr[r], rpn[r]);
+				if (rtot[r] > 64) {  // rare: deal the rest now
+					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;
+					const int32_t inc = wave_incl_scan(nc);
+					for (int32_t t0 = 64; t0 < rtot[r]; t0 += 64) {
+						const int32_t t = t0 + lane;
+						const int32_t lo = piece_owner(inc, t);
+						const int32_t k = GC + t - (__shfl(inc, lo) - __shfl(nc, lo));
+						const int32_t osrc = __shfl(mdst - off, lo), odst = __shfl(mdst, lo);
+						const int32_t oml = __shfl(ml, lo);
+						if (t < rtot[r]) {
+							u32x4 v;
+							__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
+							ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
+						}
+					}
+				}
+				wave_lds_fence();
+				ISTAMP(D_MFAR);
+				const int32_t rml_ring = (ml > 0 && !hbm) ? ml : 0;
+				// long ring matches: dealt pieces; a round of short ones
+				// (every match at most RING_LANE_MAX bytes, e.g. dense data)
+				// keeps one lane per match -- the dealing's fixed cost
+				// (owner search, dependency masks) would dominate there
+				if (__any(rml_ring > RING_LANE_MAX))
+					ring_pieces(D, mdst, off, rml_ring);
+				else
+					ring_lanes(D, mdst, off, rml_ring, rbeg[r], rL[r]);
+			}
+		}
+#endif
 		ISTAMP(D_NEAR);
 
 		// flush whole 16-byte units of [o_batch, o_end) (the first may start

@@ -83,7 +83,9 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 
 // One word per output byte of the batch (batch-relative position a =
 // A[b] + q): RES | byte, or the encoded position of the byte it copies,
-// (source position) + 65536 -- always >= 0, and below a.
+// (source position) + 65536 -- always >= 0, and below a.  Four bytes per
+// lane: dword loads of the three copies, one 16-byte store of the words
+// (four dword stores when the block's words are not 16-byte aligned).
 __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x,
                                                    const uint8_t* __restrict__ y,
                                                    const uint8_t* __restrict__ h,
@@ -96,37 +98,34 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
 		return;
-	const uint64_t ob = desc[b].out_off;
+	const uint64_t ob = desc[b].out_off;  // 256-byte aligned slot
 	const int64_t len = st[b].out_len;
 	const int64_t ab = A[b];
 	uint32_t unres = 0;
-	for (int64_t q0 = 16 * (int64_t(blockIdx.y) * TPB + threadIdx.x); q0 < len;
-	     q0 += 16 * int64_t(gridDim.y) * TPB) {
-		const u32x4 vx = *reinterpret_cast<const GLOBAL u32x4*>(gptr(x) + ob + q0);
-		const u32x4 vy = *reinterpret_cast<const GLOBAL u32x4*>(gptr(y) + ob + q0);
-		const u32x4 vh = *reinterpret_cast<const GLOBAL u32x4*>(gptr(h) + ob + q0);
-		const uint32_t wx[4] = { vx.x, vx.y, vx.z, vx.w };
-		const uint32_t wy[4] = { vy.x, vy.y, vy.z, vy.w };
-		const uint32_t wh[4] = { vh.x, vh.y, vh.z, vh.w };
-		GLOBAL uint32_t* dst = gptr(P) + ab + q0;
-		const int32_t m = int32_t(len - q0 < 16 ? len - q0 : 16);
+	for (int64_t q0 = 4 * (int64_t(blockIdx.y) * TPB + threadIdx.x); q0 < len;
+	     q0 += 4 * int64_t(gridDim.y) * TPB) {
+		const uint32_t wx = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(x) + ob + q0);
+		const uint32_t wy = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(y) + ob + q0);
+		const uint32_t wh = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(h) + ob + q0);
+		uint32_t v[4];
 #pragma unroll
-		for (int i = 0; i < 16; ++i) {
-			if (i < m) {
-				const uint32_t bx = (wx[i >> 2] >> (8 * (i & 3))) & 255u;
-				const uint32_t by = (wy[i >> 2] >> (8 * (i & 3))) & 255u;
-				const uint32_t bh = (wh[i >> 2] >> (8 * (i & 3))) & 255u;
-				uint32_t v;
-				if (bx == by) {
-					v = RES | bx;
-				} else {
-					// history position k = bx | bh << 8 is byte k - 65536 of
-					// the block-relative output: source ab + k - 65536
-					v = uint32_t(ab + int64_t(bx | (bh << 8)));
-					++unres;
-				}
-				dst[i] = v;
-			}
+		for (int i = 0; i < 4; ++i) {
+			const uint32_t bx = (wx >> (8 * i)) & 255u, by = (wy >> (8 * i)) & 255u;
+			const uint32_t bh = (wh >> (8 * i)) & 255u;
+			const bool from_hist = bx != by && q0 + i < len;
+			// history position k = bx | bh << 8 is byte k - 65536 of the
+			// block-relative output: source ab + k - 65536, encoded + 65536
+			v[i] = from_hist ? uint32_t(ab + int64_t(bx | (bh << 8))) : (RES | bx);
+			unres += from_hist ? 1u : 0u;
+		}
+		GLOBAL uint32_t* dst = gptr(P) + ab + q0;
+		if (((ab & 3) == 0) && q0 + 4 <= len) {
+			*reinterpret_cast<GLOBAL u32x4*>(dst) = u32x4{ v[0], v[1], v[2], v[3] };
+		} else {
+#pragma unroll
+			for (int i = 0; i < 4; ++i)
+				if (q0 + i < len)
+					dst[i] = v[i];
 		}
 	}
 	wave_count(ctr, unres);
@@ -230,7 +229,9 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	const int64_t per = 16 * link::TPB;
+	// ~16 KiB of output per workgroup (each lane loops ~16 times): a
+	// million 1 KiB workgroups cost more in dispatch than in work
+	const int64_t per = 16 * 4 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
 	hipLaunchKernelGGL(link::k_link_init, dim3(nblocks, gy), dim3(link::TPB), 0, stream, x, y, h, d_desc,
 	                   d_st, d_A, nblocks, d_P, d_ctr);

@@ -202,6 +202,7 @@ _sig = {
     "lz4ada_decode_stream_alloc": ([_vp, _i64, _P(_vp), _pi64], ctypes.c_int),
     "lz4ada_buffer_free": ([_vp], None),
     "lz4ada_last_path": ([], ctypes.c_int),
+    "lz4ada_release_device_cache": ([], None),
     "lz4ada_decode_linked_device": ([_vp, ctypes.c_uint64, _vp, _i64, _i64, _vp, _i64, _pi64, _vp],
                                     ctypes.c_int),
     "lz4ada_decoded_bound": ([_vp, _i64], _i64),
@@ -399,6 +400,11 @@ def last_path() -> int:
     """PATH_* bits of the paths the last decode_frame / decode_stream call on
     this thread took (bulk independent, bulk linked, reference-exact)."""
     return _lib.lz4ada_last_path()
+
+
+def release_device_cache():
+    """Free the bulk path's cached device scratch of the calling thread."""
+    _lib.lz4ada_release_device_cache()
 
 
 def decode_blocks_device(d_frame: int, frame_len: int, d_descs: int, nblocks: int, d_out: int,

@@ -295,6 +295,10 @@ int lz4ada_decode_linked_device(const void *d_frame, uint64_t frame_len,
 #define LZ4ADA_PATH_EXACT 4
 int lz4ada_last_path(void);
 
+/* The bulk path keeps its large device scratch (output slots, linked-frame
+ * decode copies) per thread between calls; this frees the calling thread's. */
+void lz4ada_release_device_cache(void);
+
 /* Upper bound of the decoded size of a stream (sum of block maxima); -1 if
  * some frame does not index (then use the _alloc calls). */
 int64_t lz4ada_decoded_bound(const uint8_t *input, int64_t len);
