@@ -298,10 +298,10 @@ struct alignas(16) IdxLds {
 
 // Walk the chain from e (an entry at or after this lane's segment start s)
 // over the sequences starting before seg_end; returns the exit (first
-// chain position >= seg_end, or n).  A malformed sequence sets err and
-// returns seg_end as a guess: from a wrong (speculative) entry that is
-// just a dead chain, and a -1 would poison every lane after it one
-// iteration at a time.
+// chain position >= seg_end, or n).  A malformed sequence sets err (epos:
+// its position) and returns seg_end as a guess: from a wrong (speculative)
+// entry that is just a dead chain, and a -1 would poison every lane after
+// it one iteration at a time.
 //
 // Every walk rewrites the segment's NSUB records (sub-segment k = bytes
 // [s + 32k, s + 32k + 32)) in LDS: rb[k] bit j = a sequence starts at byte
@@ -309,13 +309,21 @@ struct alignas(16) IdxLds {
 // there.  The lane's last walk -- from the true entry -- leaves the exact
 // records; k_index writes them to HBM once per chunk.  An output count that
 // does not fit 16 bits goes straight to its record's high word in HBM
-// (ghi[2k]; long RLE runs).  used counts the sub-segments holding a start.
+// (ghi[2k]; long RLE runs).
+//
+// Re-walk (may_stop: the lane's previous walk, exit y_old, had no error):
+// chains are deterministic, so once this walk reaches a position the
+// previous walk started a sequence at, the rest is the previous walk.  It
+// finishes that sub-segment (its count mixes both walks' sequences) and
+// stops: later records and the exit are the previous walk's.  Chains from a
+// wrong entry merge within ~14 sequences, so a re-walk costs a fraction of
+// a segment.
 __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t s, int32_t seg_end,
                                                 int32_t n, uint32_t* rb, uint16_t* rc, uint32_t* ghi,
-                                                int32_t& used, bool& err, int32_t& epos)
+                                                bool& err, int32_t& epos, int32_t y_old,
+                                                bool may_stop)
 {
 	err = false;
-	used = 0;
 	epos = INT32_MAX;
 	auto put = [&](int32_t k, uint32_t b, uint32_t c) {
 		rb[k] = b;
@@ -326,20 +334,25 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 	int32_t p = e;
 	int32_t kc = -1, nxt = 0;  // sub-segment being counted; next record to write
 	uint32_t bm = 0, cnt = 0;
+	bool merged = false;
 	while (p < seg_end) {
 		const int32_t k = (p - s) >> 5;
 		if (k != kc) {
 			if (kc >= 0)
 				put(kc, bm, cnt);
+			if (merged)
+				return y_old;
 			for (; nxt < k; ++nxt)
 				if (nxt != kc)
 					put(nxt, 0, 0);
 			nxt = k + 1;
 			kc = k;
 			bm = cnt = 0;
-			++used;
 		}
-		bm |= 1u << ((p - s) & 31);
+		const uint32_t bit = 1u << ((p - s) & 31);
+		if (may_stop && (rb[k] & bit))
+			merged = true;  // rb[k] is still the previous walk's record
+		bm |= bit;
 		Seq q;
 		if (!parse_fast(S, p, n, q)) {
 			err = true;
@@ -351,8 +364,9 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 	}
 	if (kc >= 0)
 		put(kc, bm, cnt);
-	for (; nxt < NSUB; ++nxt)
-		put(nxt, 0, 0);
+	if (!merged)
+		for (; nxt < NSUB; ++nxt)
+			put(nxt, 0, 0);
 	return p;
 }
 
@@ -441,10 +455,15 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 		// is crossed in one step instead of one iteration per segment.
 		int32_t ein = (lane == 0) ? E : s;
 		uint32_t* ghi = reinterpret_cast<uint32_t*>(tab + (C >> 5) + NSUB * lane) + 1;
-		int32_t used = 0, epos = INT32_MAX;
+#ifdef LZ4ADA_IDX_NO_MERGE_STOP
+		constexpr bool no_stop = true;
+#else
+		constexpr bool no_stop = false;
+#endif
+		int32_t epos = INT32_MAX;
 		bool err = false;
-		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used,
-		                                   err, epos)
+		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, err,
+		                                   epos, 0, false)
 		                    : ein;
 		ISTAMP(I_WALK0);
 		for (int it = 0; it < 64; ++it) {
@@ -458,8 +477,8 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			if (changed) {
 				ein = prev;
 				if (s < n) {
-					y = walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, used, err,
-					                 epos);
+					y = walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, err, epos, y,
+					                 !err && !no_stop);
 				} else {
 					y = ein;
 					err = false;
@@ -491,6 +510,10 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			// misses and the entries crawl one lane per iteration -- and are
 			// the one-wave scalar parse's best case: decline the block (large
 			// blocks only: a short one costs a few chunks either way).
+			int32_t used = 0;  // sub-segments holding a sequence start
+			if (s < n)
+				for (int k = 0; k < NSUB; ++k)
+					used += X.rbm[lane][k] ? 1 : 0;
 			if (__shfl(wave_incl_scan(used), 63) < CHUNK / SUB / 4)
 				bad = true;
 		}

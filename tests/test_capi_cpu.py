@@ -142,3 +142,20 @@ def test_decode_without_gpu_fails_loudly():
         while pos < len(data):
             c, f, l = ctx.update(data, buf, pos)
             pos += c
+
+
+def test_cli_counterparts_built_and_fail_loudly_without_gpu():
+    """unlz4ada / xxhash32ada (the reference's CLIs over the C-ABI) exist;
+    without a GPU they report the device error instead of decoding on the
+    CPU."""
+    import subprocess
+    from conftest import PKG
+    for exe in ("unlz4ada", "xxhash32ada"):
+        path = os.path.join(PKG, exe)
+        assert os.access(path, os.X_OK), path
+    if lz4ada.device_available():
+        pytest.skip("a GPU is present (tests/test_gpu_cli.py covers the CLIs)")
+    p = subprocess.run([os.path.join(PKG, "unlz4ada")], input=read_vector("z100", "lz4"),
+                       capture_output=True, timeout=60)
+    assert p.returncode == 1 and p.stdout == b""
+    assert p.stderr.decode().startswith("raised LZ4ADA.DEVICE_ERROR : ")
