@@ -777,6 +777,13 @@ __device__ __forceinline__ void ostore(DecLds& L, int32_t x, u32x4 v, int32_t n)
 	}
 }
 
+// Bytes to store of a literal piece with `left` run bytes from its start:
+// a short last piece may spill into its own match (ml bytes, stored later).
+__device__ __forceinline__ int32_t lit_width(int32_t left, int32_t ml)
+{
+	return (left >= 16 || 16 - left <= ml) ? 16 : left;
+}
+
 __device__ __forceinline__ u32x4 oload16(const DecLds& L, int32_t x)
 {
 	return ring16(L.oring, uint32_t(x) & OMASK, OMASK);
@@ -1309,7 +1316,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 
 		// L: literals (input ring -> output ring).  Short runs lane by lane;
 		// a round with a run over 32 bytes deals its 16-byte pieces over the
-		// whole wave instead.
+		// whole wave instead.  A run's last piece stores all 16 bytes when
+		// the bytes past the run lie in its own match (written in M, after
+		// every literal): one ds_write_b128 instead of up to four partial
+		// stores.
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
 			if (64 * r < N) {
@@ -1327,12 +1337,13 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 						const int32_t L = __shfl(rL[r], lo);
 						const int32_t lit = __shfl(rlit[r], lo);
 						const int32_t dst = __shfl(rdst[r], lo);
+						const int32_t ml = __shfl(rml[r], lo);
 						if (t < tot)
-							ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, L - 16 * k));
+							ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), lit_width(L - 16 * k, ml));
 					}
 				} else {
 					for (int32_t c = 0; c < rL[r]; c += 16)
-						ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), min(16, rL[r] - c));
+						ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), lit_width(rL[r] - c, rml[r]));
 				}
 			}
 		}
