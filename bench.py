@@ -260,6 +260,52 @@ def bench_linked(dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, c
             "golden": "per-block XXH32 of the output vs the generator"}
 
 
+def bench_64k(dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, unique=64):
+    """configs[1]: a 1 GiB frame of 64 KiB independent blocks with a content
+    checksum.  The decode launch (block checksums + decode, device-resident)
+    is timed with HIP events; the frame-wide content XXH32 (one serial chain,
+    SURVEY H2) runs through the D2H + host-chain pipeline and is reported
+    beside it."""
+    recs = make_unique_blocks(lz4ada.GEN_KINDS[kind], unique, bmax)
+    d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = build_shard(recs, 0, nblocks, bmax, dev)
+    d_out = torch.empty(nblocks * bmax, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nblocks * 32, dtype=torch.uint8, device=dev)
+    d_hash = torch.zeros(nblocks, dtype=torch.int32, device=dev)
+    fp, dp, op, sp = d_frame.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), d_st.data_ptr()
+    lz4ada.decode_blocks_device(fp, frame_len, dp, nblocks, op, sp, sh)
+    torch.cuda.synchronize()
+    st = check_statuses(d_st, nblocks)
+    assert all(s.code == 0 and s.cksum == descs[i].cksum for i, s in enumerate(st)), "64 KiB frame"
+    lz4ada.output_checksums_device(op, dp, sp, nblocks, d_hash.data_ptr(), sh)
+    torch.cuda.synchronize()
+    assert [h & 0xffffffff for h in d_hash.cpu().tolist()] == exp_hash, "64 KiB frame output"
+    reps = 5
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record(stream)
+    for _ in range(reps):
+        lz4ada.launch_block_checksums(fp, dp, nblocks, sp, sh)
+    e1.record(stream)
+    for _ in range(reps):
+        lz4ada.launch_decode(fp, frame_len, dp, nblocks, op, sp, sh)
+    e2.record(stream)
+    torch.cuda.synchronize()
+    ck_ms, dec_ms = e0.elapsed_time(e1) / reps, e1.elapsed_time(e2) / reps
+    h = lz4ada.XXHash32()
+    t0 = time.perf_counter()
+    h.update_device_d2h(op, raw, None, sh)
+    t_hash = time.perf_counter() - t0
+    assert h.final() == content_hash(recs, nblocks), "64 KiB frame content checksum"
+    del d_frame, d_out
+    return {"workload": f"configs[1]: {raw >> 30} GiB frame, {nblocks} x 64 KiB independent "
+                        f"{kind} blocks, FLG 0x74 (B.Indep|B.Checksum|C.Checksum)",
+            "decode_ms": round(dec_ms, 3), "checksum_ms": round(ck_ms, 3),
+            "MiB_s": round(raw / ((dec_ms + ck_ms) * 1e-3) / MiB, 1),
+            "frac": round((comp + raw) / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "content_xxh32_s": round(t_hash, 3),
+            "e2e_MiB_s": round(raw / ((dec_ms + ck_ms) * 1e-3 + t_hash) / MiB, 1),
+            "compressed_bytes": comp, "decoded_bytes": raw}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -275,6 +321,8 @@ def main():
     ap.add_argument("--classes", default="", help="extra classes to time, e.g. dense,rle,literal")
     ap.add_argument("--no-linked", action="store_true",
                     help="skip the configs[4] row (1 GiB linked frame, 256 KiB blocks)")
+    ap.add_argument("--no-64k", action="store_true",
+                    help="skip the configs[1] row (1 GiB frame, 64 KiB blocks)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_decode.json"))
     args = ap.parse_args()
 
@@ -440,6 +488,9 @@ def main():
     # every block at once against synthetic history, resolved on the GPU
     if rank == 0 and not args.no_linked:
         result["linked_c5"] = bench_linked(dev, sh, stream)
+    # ---- configs[1]: 1 GiB of 64 KiB independent blocks + content checksum
+    if rank == 0 and not args.no_64k:
+        result["c2_64k"] = bench_64k(dev, sh, stream)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(recs, bmax, args.cpu_budget)

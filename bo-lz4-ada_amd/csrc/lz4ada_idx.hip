@@ -777,13 +777,6 @@ __device__ __forceinline__ void ostore(DecLds& L, int32_t x, u32x4 v, int32_t n)
 	}
 }
 
-// Bytes to store of a literal piece with `left` run bytes from its start:
-// a short last piece may spill into its own match (ml bytes, stored later).
-__device__ __forceinline__ int32_t lit_width(int32_t left, int32_t ml)
-{
-	return (left >= 16 || 16 - left <= ml) ? 16 : left;
-}
-
 __device__ __forceinline__ u32x4 oload16(const DecLds& L, int32_t x)
 {
 	return ring16(L.oring, uint32_t(x) & OMASK, OMASK);
@@ -900,6 +893,26 @@ __device__ __forceinline__ int32_t pattern_step(int32_t off)
 
 __device__ __forceinline__ int32_t piece_owner(int32_t inc, int32_t t);
 
+// Owner lane of piece t0 + lane, lane i holding pieces [inc_i - np_i,
+// inc_i) (inc: inclusive prefix sum, monotone): each lane marks its first
+// piece's slot of the 64-piece chunk in LDS, a prefix maximum fills the
+// slots in between, and the chunk's first slot is seeded with the owner of
+// piece t0 (the lanes with inc <= t0, counted from a ballot).  Two LDS
+// round trips instead of six dependent shuffles of a binary search.
+__device__ __forceinline__ int32_t chunk_owner(DecLds& D, int32_t inc, int32_t np, int32_t t0)
+{
+	const int32_t lane = int32_t(lane_id());
+	const int32_t seed = __popcll(__ballot(inc <= t0));
+	D.own[lane] = uint8_t(lane == 0 ? seed : 0);
+	const int32_t excl = inc - np;
+	if (np > 0 && excl >= t0 && excl < t0 + 64)
+		D.own[excl - t0] = uint8_t(lane);
+	wave_lds_fence();
+	const int32_t v = D.own[lane];
+	wave_lds_fence();  // own[] is marked again for the next chunk
+	return wave_incl_max(v);
+}
+
 // Every lane's match (dst, off, ml; ml = 0: none) with a source in the LDS
 // ring, cut into pieces dealt over the wave: 16 output bytes each, or stp
 // bytes of a period-off pattern (off < 16 < ml would overlap: match byte i
@@ -918,7 +931,7 @@ __device__ __forceinline__ void ring_pieces(DecLds& D, int32_t mdst, int32_t off
 	for (int32_t t0 = 0; t0 < tot; t0 += 64) {
 		const int32_t t = t0 + lane;
 		const bool act = t < tot;
-		const int32_t lo = piece_owner(inc, act ? t : tot - 1);
+		const int32_t lo = min(chunk_owner(D, inc, np, t0), 63);
 		const int32_t k = t - (__shfl(inc, lo) - __shfl(np, lo));
 		const int32_t od = __shfl(mdst, lo), ooff = __shfl(off, lo), oml = __shfl(ml, lo);
 		const int32_t ostp = __shfl(stp, lo);
@@ -1316,10 +1329,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 
 		// L: literals (input ring -> output ring).  Short runs lane by lane;
 		// a round with a run over 32 bytes deals its 16-byte pieces over the
-		// whole wave instead.  A run's last piece stores all 16 bytes when
-		// the bytes past the run lie in its own match (written in M, after
-		// every literal): one ds_write_b128 instead of up to four partial
-		// stores.
+		// whole wave instead.  (Storing a short last piece as 16 bytes that
+		// spill into its own match, rewritten in M, measured no faster.)
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
 			if (64 * r < N) {
@@ -1332,18 +1343,17 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					const int32_t tot = __shfl(inc, 63);
 					for (int32_t t0 = 0; t0 < tot; t0 += 64) {
 						const int32_t t = t0 + lane;
-						const int32_t lo = piece_owner(inc, t);
+						const int32_t lo = min(chunk_owner(D, inc, nc, t0), 63);
 						const int32_t k = t - (__shfl(inc, lo) - __shfl(nc, lo));
 						const int32_t L = __shfl(rL[r], lo);
 						const int32_t lit = __shfl(rlit[r], lo);
 						const int32_t dst = __shfl(rdst[r], lo);
-						const int32_t ml = __shfl(rml[r], lo);
 						if (t < tot)
-							ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), lit_width(L - 16 * k, ml));
+							ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, L - 16 * k));
 					}
 				} else {
 					for (int32_t c = 0; c < rL[r]; c += 16)
-						ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), lit_width(rL[r] - c, rml[r]));
+						ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), min(16, rL[r] - c));
 				}
 			}
 		}
