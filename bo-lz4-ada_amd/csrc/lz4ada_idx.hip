@@ -943,20 +943,23 @@ __device__ __forceinline__ void ring_pieces(DecLds& D, int32_t mdst, int32_t off
 		const int32_t s_lo = (opat || wide) ? od - ooff : od - ooff + 16 * k;
 		const int32_t s_hi = (opat || wide) ? od : s_lo + pn;
 		// lanes of this chunk whose piece [pd, pd + 16) meets [s_lo, s_hi):
-		// pd is monotone over the lanes, so two binary searches
+		// pd is monotone over the lanes, so two binary searches -- skipped
+		// when every source ends before the chunk's first piece
 		const int32_t pe = act ? pd + 16 : INT32_MAX, ps = act ? pd : INT32_MAX;
-		int32_t j1 = 0, c2 = 0;
-#pragma unroll
-		for (int st = 32; st >= 1; st >>= 1) {
-			if (__shfl(pe, j1 + st - 1) <= s_lo)
-				j1 += st;
-			if (__shfl(ps, c2 + st - 1) < s_hi)
-				c2 += st;
-		}
-		const int32_t j2 = min(c2 - 1, lane - 1);
 		uint64_t dep = 0;
-		if (act && j1 <= j2)
-			dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
+		if (!__all(!act || s_hi <= __shfl(ps, 0))) {
+			int32_t j1 = 0, c2 = 0;
+#pragma unroll
+			for (int st = 32; st >= 1; st >>= 1) {
+				if (__shfl(pe, j1 + st - 1) <= s_lo)
+					j1 += st;
+				if (__shfl(ps, c2 + st - 1) < s_hi)
+					c2 += st;
+			}
+			const int32_t j2 = min(c2 - 1, lane - 1);
+			if (act && j1 <= j2)
+				dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
+		}
 		bool pend = act;
 		for (;;) {
 			const uint64_t pm = __ballot(pend);

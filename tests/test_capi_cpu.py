@@ -159,3 +159,54 @@ def test_cli_counterparts_built_and_fail_loudly_without_gpu():
                        capture_output=True, timeout=60)
     assert p.returncode == 1 and p.stdout == b""
     assert p.stderr.decode().startswith("raised LZ4ADA.DEVICE_ERROR : ")
+
+
+def _hdrinfo_expected(data: bytes) -> str:
+    """tool_lz4hdrinfo/lz4hdrinfo.adb:70-145 restated (test side).  The tool
+    reads one 64-byte buffer; bytes past a short input (undefined in the
+    Ada tool) read as 0 in the counterpart."""
+    data = (data + bytes(64))[:64]
+    lines = ["Ma_Sys.ma LZ4 Header Info 1.0.0, (c) 2023 Ma_Sys.ma <info@masysma.net>", ""]
+    magic = struct.unpack("<I", data[:4])[0]
+    tf = lambda b: "TRUE" if b else "FALSE"
+    if magic == 0x184D2204:
+        flg, bd = data[4], data[5]
+        bms = (bd & 0x70) >> 4
+        lines += [f"Declared Format        = {magic:08x} (modern)", f"FLG                    = {flg:02x}",
+                  f"    Version:64|128     = {(flg & 0xc0) >> 6:02x}",
+                  f"    Block_Checksum:16  = {tf(flg & 16)}", f"    Content_Size:8     = {tf(flg & 8)}",
+                  f"    Content_Checksum:4 = {tf(flg & 4)}", f"    Reserved:2         = {tf(flg & 2)}",
+                  f"    Dictionary_ID:1    = {tf(flg & 1)}", f"BD                     = {bd:02x}",
+                  f"    Has_Reserved       = {tf(bd & 0x8f)}",
+                  "    Block_Max_Size     = " + {4: "64 KiB", 5: "256 KiB", 6: "1 MiB",
+                                                 7: "4 MiB"}.get(bms, "INVALID") + f" ({bms:02x})"]
+        cur = 6
+        if flg & 8:
+            lines.append(f"Content_Size           =  {struct.unpack('<Q', data[cur:cur + 8])[0]}")
+            cur += 8
+        cur += 4 if flg & 1 else 0
+        lines.append(f"Header_Checksum        = {data[cur]:02x}")
+    elif magic == 0x184C2102:
+        lines.append(f"Declared Format        = {magic:08x} (legacy)")
+    elif 0x184D2A50 <= magic <= 0x184D2A5F:
+        lines += [f"Declared Format        = {magic:08x} (skippable)",
+                  f"Content_Size           =  {struct.unpack('<I', data[4:8])[0]}"]
+    else:
+        lines.append(f"Declared Format        = {magic:08x} (UNSUPPORTED)")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("name", good_vectors() + error_vectors())
+def test_lz4hdrinfo(name):
+    """The header dumper counterpart (host only, no library) on every vector."""
+    import subprocess
+    from conftest import PKG
+    ext = "lz4" if name in good_vectors() else "err"
+    data = read_vector(name, ext)
+    p = subprocess.run([os.path.join(PKG, "lz4hdrinfo")], input=data, capture_output=True, timeout=30)
+    if len(data) < 7:
+        assert p.returncode == 1
+        assert p.stderr.decode().startswith("raised CONSTRAINT_ERROR : Partial frame detected.")
+    else:
+        assert p.returncode == 0
+        assert p.stdout.decode() == _hdrinfo_expected(data)

@@ -54,3 +54,35 @@ def test_xxhash32ada():
     assert p.stdout.decode() == "xxhash32(0, stdin) = 0x%08x\n" % O.xxh32(data)
     p = run(XXH, b"")
     assert p.stdout.decode() == "xxhash32(0, stdin) = 0x02cc5d05\n"
+
+
+UNLZ4S = os.path.join(PKG, "unlz4ada_simple")
+
+
+@pytest.mark.parametrize("name", good_vectors())
+def test_unlz4ada_simple_good_vectors(name, digests):
+    """tool_unlz4ada_simple: Init(For_All) + Update over 4 KiB reads (the
+    streaming facade on the GPU), every vector incl. concatenated frames."""
+    p = run(UNLZ4S, read_vector(name, "lz4"))
+    assert p.returncode == 0, p.stderr.decode()
+    assert hashlib.sha256(p.stdout).hexdigest() == digests[name]["sha256"]
+
+
+@pytest.mark.parametrize("name", error_vectors())
+def test_unlz4ada_simple_error_vectors(name):
+    data = read_vector(name, "err")
+    st, ref, eof, msg = O.decode_stream(data, chunk=4096, reservation=O.FOR_ALL)
+    p = run(UNLZ4S, data)
+    if st == O.OK:
+        # For_All accepts what Single_Frame rejects (e.g. trailing bytes as a
+        # next frame); then the tool's own end-of-input check decides
+        assert p.stdout == ref
+        if eof == O.EOF_NO:
+            assert p.returncode == 1
+            assert p.stderr.decode().strip() == "raised CONSTRAINT_ERROR : Input ended mid-frame."
+        else:
+            assert p.returncode == 0
+    else:
+        assert p.returncode == 1
+        assert p.stderr.decode().strip() == O.exception_information(st, msg)
+        assert ref.startswith(p.stdout)
