@@ -104,6 +104,10 @@ __device__ __forceinline__ uint32_t fetch4(const Src& S, int32_t p)
 	for (int i = 0; i < 4; ++i)
 		if (g + i < S.lim)
 			v |= uint32_t(*reinterpret_cast<cg8*>(g + i)) << (8 * i);
+	// settle this rare path's loads here: left pending, they make every
+	// merge after it (the walk loops' heads) wait for all memory, the
+	// in-flight next-chunk prefetch included
+	__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 	return v;
 }
 
@@ -145,6 +149,10 @@ __device__ __forceinline__ u32x4 fetch16(const Src& S, int32_t p)
 			t[i] = (g + i < S.lim) ? *reinterpret_cast<cg8*>(g + i) : 0;
 		__builtin_memcpy(&v, t, 16);
 	}
+	// settle the rare global read here (see fetch4): otherwise every use of
+	// the LDS path's result waits for all memory -- the batch's in-flight
+	// HBM match loads and flush stores included
+	__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 	return v;
 }
 
