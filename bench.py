@@ -280,16 +280,20 @@ def bench_64k(dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, uniq
     torch.cuda.synchronize()
     assert [h & 0xffffffff for h in d_hash.cpu().tolist()] == exp_hash, "64 KiB frame output"
     reps = 5
-    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0, e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
     e0.record(stream)
     for _ in range(reps):
-        lz4ada.launch_block_checksums(fp, dp, nblocks, sp, sh)
+        lz4ada.decode_blocks_device(fp, frame_len, dp, nblocks, op, sp, sh)
     e1.record(stream)
     for _ in range(reps):
-        lz4ada.launch_decode(fp, frame_len, dp, nblocks, op, sp, sh)
+        lz4ada.launch_block_checksums(fp, dp, nblocks, sp, sh)
     e2.record(stream)
+    for _ in range(reps):
+        lz4ada.launch_decode(fp, frame_len, dp, nblocks, op, sp, sh)
+    e3.record(stream)
     torch.cuda.synchronize()
-    ck_ms, dec_ms = e0.elapsed_time(e1) / reps, e1.elapsed_time(e2) / reps
+    step_ms = e0.elapsed_time(e1) / reps
+    ck_ms, dec_ms = e1.elapsed_time(e2) / reps, e2.elapsed_time(e3) / reps
     h = lz4ada.XXHash32()
     t0 = time.perf_counter()
     h.update_device_d2h(op, raw, None, sh)
@@ -298,11 +302,12 @@ def bench_64k(dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, uniq
     del d_frame, d_out
     return {"workload": f"configs[1]: {raw >> 30} GiB frame, {nblocks} x 64 KiB independent "
                         f"{kind} blocks, FLG 0x74 (B.Indep|B.Checksum|C.Checksum)",
-            "decode_ms": round(dec_ms, 3), "checksum_ms": round(ck_ms, 3),
-            "MiB_s": round(raw / ((dec_ms + ck_ms) * 1e-3) / MiB, 1),
-            "frac": round((comp + raw) / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "step_ms": round(step_ms, 3), "decode_alone_ms": round(dec_ms, 3),
+            "checksum_alone_ms": round(ck_ms, 3),
+            "MiB_s": round(raw / (step_ms * 1e-3) / MiB, 1),
+            "frac": round((comp + raw) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "content_xxh32_s": round(t_hash, 3),
-            "e2e_MiB_s": round(raw / ((dec_ms + ck_ms) * 1e-3 + t_hash) / MiB, 1),
+            "e2e_MiB_s": round(raw / (step_ms * 1e-3 + t_hash) / MiB, 1),
             "compressed_bytes": comp, "decoded_bytes": raw}
 
 
@@ -363,15 +368,13 @@ def main():
         f"{raw_bytes / MiB:.0f} MiB decoded")
 
     def step(events=None):
-        if events is None:
-            lz4ada.decode_blocks_device(fp, frame_len, dp, nb, op, sp, sh)
-            return
-        e0, e1, e2 = events
-        e0.record(stream)
-        lz4ada.launch_block_checksums(fp, dp, nb, sp, sh)
-        e1.record(stream)
-        lz4ada.launch_decode(fp, frame_len, dp, nb, op, sp, sh)
-        e2.record(stream)
+        # the product call: block checksums on the library's side stream
+        # beside the decoder's first pass, joined back into `stream`
+        if events is not None:
+            events[0].record(stream)
+        lz4ada.decode_blocks_device(fp, frame_len, dp, nb, op, sp, sh)
+        if events is not None:
+            events[1].record(stream)
 
     for _ in range(args.warmup):
         step()
@@ -388,8 +391,8 @@ def main():
     log("[bench] golden check passed (per-block XXH32 of output, block checksums)")
 
     # ---- timed region: exactly K steps
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -399,10 +402,22 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed)
-    ck_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / args.steps
-    dec_ms = sum(b.elapsed_time(c) for _, b, c in evs) / args.steps
+    dec_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     st = check_statuses(d_status, nb)
     assert all(s.code == 0 for s in st)
+    # the two halves alone (after the timed region, same stream): what the
+    # overlap hides
+    alone = {}
+    for name, fn in (("block_checksums", lambda: lz4ada.launch_block_checksums(fp, dp, nb, sp, sh)),
+                     ("decode", lambda: lz4ada.launch_decode(fp, frame_len, dp, nb, op, sp, sh))):
+        a_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(3)]
+        for a, b in a_ev:
+            a.record(stream)
+            fn()
+            b.record(stream)
+        torch.cuda.synchronize()
+        alone[name] = round(sum(a.elapsed_time(b) for a, b in a_ev) / len(a_ev), 3)
 
     ms_per_step = elapsed / args.steps * 1e3
     total_raw = raw_bytes * world * args.steps
@@ -420,8 +435,11 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "kernel": dec_kernel, "kernel_ms": round(dec_ms, 3),
+            "kernel_ms_note": "HIP events around lz4ada_decode_blocks_device on its stream: "
+                              "k_index + k_decode_idx with k_xxh32_rows (block checksums) "
+                              "overlapped on the side stream",
             "alg_bytes_per_launch": alg_bytes,
-            "checksum_kernel": "k_block_checksums", "checksum_kernel_ms": round(ck_ms, 3)}
+            "alone_ms": alone}
 
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "MiB/s", "n_gpus": world,

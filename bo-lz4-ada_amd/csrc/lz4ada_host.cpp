@@ -1463,9 +1463,8 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 		d_st.reserve(nb);
 		HIP_OK(hipMemcpy(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc), hipMemcpyHostToDevice));
 		HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
-		HIP_OK(launch_block_checksums(d_frame, d_desc.p, nb, d_st.p, stream));
-		HIP_OK(launch_decode_blocks(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out, d_st.p,
-		                            stream));
+		HIP_OK(launch_decode_checked(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out, d_st.p,
+		                             stream));
 		std::vector<lz4ada_block_status> st(nb);
 		HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status), hipMemcpyDeviceToHost));
 		bool pre = false;
@@ -1822,11 +1821,9 @@ int lz4ada_decode_blocks_device(const void* d_frame, uint64_t frame_len,
                                 lz4ada_block_status* d_status, void* stream)
 {
 	return guarded(nullptr, [&] {
-		hipStream_t s = static_cast<hipStream_t>(stream);
-		HIP_OK(launch_block_checksums(static_cast<const uint8_t*>(d_frame), d_descs,
-		                              uint32_t(nblocks), d_status, s));
-		HIP_OK(launch_decode_blocks(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
-		                            uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status, s));
+		HIP_OK(launch_decode_checked(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
+		                             uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,
+		                             static_cast<hipStream_t>(stream)));
 	});
 }
 

@@ -122,6 +122,14 @@ hipError_t launch_block_checksums(const uint8_t* d_frame,
                                   const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                   lz4ada_block_status* d_status, hipStream_t stream);
 
+// Block checksums and the default decoder together: the checksum kernel
+// (latency-bound, no LDS) runs on a side stream beside pass 1 of the
+// index-driven decoder, fork and join by events; `stream` sees both done.
+hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                 uint8_t* d_out, lz4ada_block_status* d_status,
+                                 hipStream_t stream);
+
 // Per-block XXH32 of decoded output slots (golden checks).
 hipError_t launch_output_checksums(const uint8_t* d_out,
                                    const lz4ada_block_desc* d_desc, uint32_t nblocks,

@@ -21,9 +21,11 @@
 //    output.  Long or unusual tokens (multi-byte length extensions, runs
 //    over 256 B, anything malformed) go through a wave-cooperative
 //    one-token path that also produces the precise error.
-//  * k_block_checksums / k_xxh32_update -- XXH32 with the four accumulator
-//    lanes mapped onto lanes 0-3 of a wavefront; all 64 lanes load and
-//    pre-multiply 256 B per step, ds_bpermute feeds the serial chain.
+//  * k_xxh32_rows -- per-block XXH32 (block checksums, output hashes), four
+//    blocks per wave, the chain walking a 16-lane row's quads by DPP.
+//  * k_xxh32_update -- streaming XXH32 of one buffer with the four
+//    accumulator lanes mapped onto lanes 0-3 of a wavefront; all 64 lanes
+//    load and pre-multiply 256 B per step, ds_bpermute feeds the chain.
 //  * k_serial_block -- reference-exact single-lane emulation of one block
 //    on a device mirror of the caller's Buffer (Output_Pos wrap, history,
 //    8-byte wild-copy overshoot and its D1 side effect).  Used by the
@@ -31,6 +33,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+
+#include <utility>
 
 #include "lz4ada_internal.h"
 #include "lz4ada_dev.h"
@@ -162,51 +166,192 @@ __device__ uint32_t xxh32_final_dev(uint32_t v0, uint32_t v1, uint32_t v2, uint3
 	return ret ^ (ret >> 16);
 }
 
-// One-shot XXH32 (seed 0) of [p, p+n) by a whole wave (XXHash32.Hash).
-__device__ uint32_t wave_xxh32(cg8* p, uint64_t n)
+// ------------------------------------------------- XXH32, four blocks a wave
+// The stripe chain is serial (acc = rotl(acc + w P2, 13) P1: three dependent
+// VALU ops), so one block per wave leaves 60 of 64 lanes idle.
+// k_xxh32_rows gives each 16-lane row its own block.  Lane 4m + a of a row
+// loads word a of stripe 4t + m (register t: 16 consecutive words), so the
+// row's four quads hold four consecutive stripes.  The chain walks the
+// quads: sub-step k updates acc := rotl(ror4(acc) + x, 13) P1 in every lane,
+// ror4 (DPP row_ror:4) handing quad k the accumulators quad k - 1 produced
+// one sub-step earlier; only quad k's result is the chain's, the other quads
+// compute values nobody reads.  No shuffles, no LDS: three VALU per stripe
+// for four blocks.  Loads run XW registers ahead of the chain.  (Inline-asm
+// loads with hand-counted waits were tried and dropped: the compiler may
+// copy an asm load's destination before the data lands -- it faulted.)
+constexpr int XG = 4;    // blocks per wave (16-lane rows)
+#ifndef LZ4ADA_XW
+#define LZ4ADA_XW 48
+#endif
+constexpr int XW = LZ4ADA_XW;  // registers in flight (vmcnt holds 63)
+
+struct XRow {
+	cg32* q;       // aligned-down start (a valid address even for an empty row)
+	uint32_t sh;   // start misalignment, bytes
+	int32_t nw;    // words in whole stripes
+	int32_t dlast; // last whole-stripe word when sh == 0: its pair starts one word early
+};
+
+__device__ __forceinline__ int32_t xrow_w(const XRow& R, int32_t t)
+{
+	return min(16 * t + int32_t(lane_id() & 15u), max(R.nw - 1, 0));
+}
+
+// Register t's pair for this lane, clamped to the row's data: aligned dwords
+// q[w], q[w + 1] -- for an aligned start's last word (q[w + 1] could pass the
+// data's last page) q[w - 1], q[w].
+__device__ __forceinline__ uint64_t xrow_load(const XRow& R, int32_t t)
+{
+	const int32_t w = xrow_w(R, t);
+	uint64_t v;
+	__builtin_memcpy(&v, R.q + (w - (w == R.dlast ? 1 : 0)), 8);
+	return v;
+}
+
+__device__ __forceinline__ uint32_t xrow_word(const XRow& R, int32_t t, uint64_t v)
+{
+	const uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+	return xrow_w(R, t) == R.dlast ? hi : __builtin_amdgcn_alignbyte(hi, lo, R.sh);
+}
+
+// Four sub-steps over register t's stripes (lim: how many of them are the
+// row's; GUARD false: all four).
+template <bool GUARD>
+__device__ __forceinline__ uint32_t xrow_chain(uint32_t acc, uint32_t word, int32_t lim)
+{
+	const uint32_t x = word * P2;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const uint32_t prev = uint32_t(__builtin_amdgcn_update_dpp(0, int(acc), 0x124, 0xf, 0xf, false));
+		const uint32_t nacc = rotl32(prev + x, 13) * P1;  // row_ror:4 above
+		acc = (!GUARD || k < lim) ? nacc : acc;
+	}
+	return acc;
+}
+
+// One round: consume registers t0 .. t0 + XW - 1, load t0 + XW .. t0 + 2 XW - 1.
+__device__ __forceinline__ uint32_t xrow_round(const XRow& R, uint64_t (&buf)[XW], uint32_t acc,
+                                               int32_t t0, int32_t tfull, int32_t tall)
+{
+#pragma unroll
+	for (int r = 0; r < XW; ++r) {
+		const int32_t t = t0 + r;
+		const uint32_t word = xrow_word(R, t, buf[r]);
+		// the slot's old pair dies before its next load is issued, so both
+		// share registers: hoisted above the use, the load made the allocator
+		// rotate all XW slots at the loop's back edge (XW copies behind a
+		// vmcnt(0))
+		__builtin_amdgcn_sched_barrier(0);
+		buf[r] = xrow_load(R, t + XW);
+		if (t < tfull)
+			acc = xrow_chain<false>(acc, word, 4);
+		else if (t < tall)
+			acc = xrow_chain<true>(acc, word, (R.nw - 16 * t) >> 2);
+	}
+	return acc;
+}
+
+// XXH32 (seed 0, XXHash32.Hash: lz4ada.adb:979-1017) of row j's bytes
+// [p, p + n); returned in the row's lane 0.  p may be null when n == 0
+// (fallback: any valid device address).
+__device__ __forceinline__ uint32_t xxh32_rows(cg8* p, uint64_t n, cg32* fallback)
 {
 	const uint32_t lane = lane_id();
-	const uint32_t init[4] = { P1 + P2, P2, 0u, 0u - P1 };
-	uint32_t acc = init[lane & 3u];
 	const uint64_t ns = n / 16;
-	acc = wave_xxh32_stripes(acc, p, ns);
-	uint32_t v0 = __shfl(acc, 0), v1 = __shfl(acc, 1), v2 = __shfl(acc, 2),
-	         v3 = __shfl(acc, 3);
-	uint8_t tail[16];
-	const int32_t tl = int32_t(n - ns * 16);
-	for (int i = 0; i < tl; ++i)
-		tail[i] = p[ns * 16 + i];
-	return xxh32_final_dev(v0, v1, v2, v3, tail, tl, n);
+	XRow R;
+	if (ns == 0) {
+		R.q = fallback;
+		R.sh = 0;
+		R.nw = 0;
+	} else {
+		const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+		R.q = reinterpret_cast<cg32*>(a & ~uintptr_t(3));
+		R.sh = uint32_t(a & 3u);
+		R.nw = int32_t(ns * 4);
+	}
+	R.dlast = (R.sh == 0 && R.nw > 0) ? R.nw - 1 : -1;
+	int32_t tall = (R.nw + 15) >> 4, tfull = R.nw >> 4;
+#pragma unroll
+	for (int s = 16; s <= 32; s <<= 1) {
+		tall = max(tall, __shfl_xor(tall, s));
+		tfull = min(tfull, __shfl_xor(tfull, s));
+	}
+	tall = __builtin_amdgcn_readfirstlane(tall);  // wave-uniform: scalar loop bounds
+	tfull = __builtin_amdgcn_readfirstlane(tfull);
+	const uint32_t init[4] = { P1 + P2, P2, 0u, 0u - P1 };
+	uint32_t acc = init[lane & 3u];  // every quad: sub-step 0 reads quad 3
+	// settle the descriptor loads first: left pending into the chain loop,
+	// the wait pass merges them into the loop head as a vmcnt(0) -- every
+	// round, for the XW loads in flight too
+	__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+	// the prologue in slot order (scheduled freely, it came out reversed,
+	// and the loop head then waited vmcnt(0) for slot 0)
+	uint64_t buf[XW];
+#pragma unroll
+	for (int r = 0; r < XW; ++r) {
+		buf[r] = xrow_load(R, r);
+		__builtin_amdgcn_sched_barrier(0);
+	}
+	for (int32_t t0 = 0; t0 < tall; t0 += XW)
+		acc = xrow_round(R, buf, acc, t0, tfull, tall);
+	// the chain's last sub-step ran in quad (ns - 1) mod 4
+	const int src = int(lane & 48u) | int(((uint32_t(ns) + 3u) & 3u) << 2);
+	const uint32_t v0 = __shfl(acc, src), v1 = __shfl(acc, src + 1), v2 = __shfl(acc, src + 2),
+	               v3 = __shfl(acc, src + 3);
+	uint32_t h = uint32_t(n);
+	if ((lane & 15u) == 0) {
+		h += n >= 16 ? rotl32(v0, 1) + rotl32(v1, 7) + rotl32(v2, 12) + rotl32(v3, 18) : P5;
+		cg8* t = p + ns * 16;
+		const int32_t tl = int32_t(n - ns * 16);
+		int32_t d = 0;
+		for (; d + 4 <= tl; d += 4) {
+			const uint32_t w = uint32_t(t[d]) | (uint32_t(t[d + 1]) << 8) |
+			                   (uint32_t(t[d + 2]) << 16) | (uint32_t(t[d + 3]) << 24);
+			h = rotl32(h + w * P3, 17) * P4;
+		}
+		for (; d < tl; ++d)
+			h = rotl32(h + uint32_t(t[d]) * P5, 11) * P1;
+		h = (h ^ (h >> 15)) * P2;
+		h = (h ^ (h >> 13)) * P3;
+		h ^= h >> 16;
+	}
+	return h;
 }
 
-__global__ __launch_bounds__(64) void k_block_checksums(const uint8_t* __restrict__ frame,
-                                                         const lz4ada_block_desc* __restrict__ desc,
-                                                         uint32_t nblocks,
-                                                         lz4ada_block_status* __restrict__ st)
+// out == nullptr: block checksums of the compressed data (blocks with
+// B.Checksum; st[b].cksum).  Else: XXH32 of each block's decoded output
+// (st[b].out_len bytes at out + out_off) into hash[b].
+__global__ __launch_bounds__(64) void k_xxh32_rows(const uint8_t* __restrict__ frame,
+                                                   const uint8_t* __restrict__ out,
+                                                   const lz4ada_block_desc* __restrict__ desc,
+                                                   uint32_t nblocks,
+                                                   lz4ada_block_status* __restrict__ st,
+                                                   uint32_t* __restrict__ hash)
 {
-	const uint32_t b = blockIdx.x;
-	if (b >= nblocks)
-		return;
-	const lz4ada_block_desc d = desc[b];
-	if (!(d.flags & LZ4ADA_BLOCK_HAS_CKSUM))
-		return;
-	uint32_t h = wave_xxh32(gptr(frame) + d.in_off, d.in_len);
-	if (lane_id() == 0)
-		st[b].cksum = h;
-}
-
-__global__ __launch_bounds__(64) void k_output_checksums(const uint8_t* __restrict__ out,
-                                                          const lz4ada_block_desc* __restrict__ desc,
-                                                          uint32_t nblocks,
-                                                          const lz4ada_block_status* __restrict__ st,
-                                                          uint32_t* __restrict__ hash)
-{
-	const uint32_t b = blockIdx.x;
-	if (b >= nblocks)
-		return;
-	uint32_t h = wave_xxh32(gptr(out) + desc[b].out_off, st[b].out_len);
-	if (lane_id() == 0)
-		hash[b] = h;
+	const uint32_t lane = lane_id();
+	const uint32_t b = blockIdx.x * XG + (lane >> 4);
+	cg8* p = nullptr;
+	uint64_t n = 0;
+	bool want = false;
+	if (b < nblocks) {
+		const lz4ada_block_desc d = desc[b];
+		if (out) {
+			p = gptr(out) + d.out_off;
+			n = st[b].out_len;
+			want = true;
+		} else if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM) {
+			p = gptr(frame) + d.in_off;
+			n = d.in_len;
+			want = true;
+		}
+	}
+	const uint32_t h = xxh32_rows(p, n, reinterpret_cast<cg32*>(gptr(desc)));
+	if (want && (lane & 15u) == 0) {
+		if (out)
+			hash[b] = h;
+		else
+			st[b].cksum = h;
+	}
 }
 
 // Streaming XXHash32.Update (lz4ada.adb:942-977) on a device-resident state.
@@ -2059,10 +2204,18 @@ hipError_t launch_decode_pc(const uint8_t* d_frame, uint64_t frame_len,
 	return hipGetLastError();
 }
 
+static int decoder_variant();
+
 hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                 uint8_t* d_out, lz4ada_block_status* d_status,
                                 hipStream_t stream)
+{
+	return launch_decode_variant(d_frame, frame_len, d_desc, nblocks, d_out, d_status,
+	                             decoder_variant(), stream);
+}
+
+static int decoder_variant()
 {
 	// Default: the index-driven decoder (lz4ada_idx.hip), the two-wave
 	// decoder for the blocks it declines.  LZ4ADA_DECODER=pc / wave / wg
@@ -2077,8 +2230,91 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
 			return int(DEC_WAVE);
 		return int(DEC_IDX);
 	}();
-	return launch_decode_variant(d_frame, frame_len, d_desc, nblocks, d_out, d_status, variant,
-	                             stream);
+	return variant;
+}
+
+// A side stream and its fork / join events per device and host thread,
+// created on first use and kept for the process.
+struct SideStream {
+	hipStream_t s = nullptr;
+	hipEvent_t fork = nullptr, join = nullptr;
+};
+
+static hipError_t side_stream(SideStream*& out)
+{
+	constexpr int MAXDEV = 64;
+	static thread_local SideStream cache[MAXDEV];
+	int dev = 0;
+	hipError_t err = hipGetDevice(&dev);
+	if (err != hipSuccess)
+		return err;
+	if (dev < 0 || dev >= MAXDEV)
+		return hipErrorInvalidDevice;
+	SideStream& c = cache[dev];
+	if (!c.s) {
+		SideStream n;
+		err = hipStreamCreateWithFlags(&n.s, hipStreamNonBlocking);
+		if (err == hipSuccess)
+			err = hipEventCreateWithFlags(&n.fork, hipEventDisableTiming);
+		if (err == hipSuccess)
+			err = hipEventCreateWithFlags(&n.join, hipEventDisableTiming);
+		if (err != hipSuccess) {
+			if (n.join)
+				(void)hipEventDestroy(n.join);
+			if (n.fork)
+				(void)hipEventDestroy(n.fork);
+			if (n.s)
+				(void)hipStreamDestroy(n.s);
+			return err;
+		}
+		c = n;
+	}
+	out = &c;
+	return hipSuccess;
+}
+
+hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
+                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
+                                 uint8_t* d_out, lz4ada_block_status* d_status,
+                                 hipStream_t stream)
+{
+	if (nblocks == 0)
+		return hipSuccess;
+	if (decoder_variant() != DEC_IDX || getenv("LZ4ADA_NO_OVERLAP")) {
+		hipError_t err = launch_block_checksums(d_frame, d_desc, nblocks, d_status, stream);
+		return err != hipSuccess ? err
+		                         : launch_decode_blocks(d_frame, frame_len, d_desc, nblocks, d_out,
+		                                                d_status, stream);
+	}
+	// k_index (2 waves/SIMD, LDS-bound, 168 VGPRs) leaves VGPRs for one
+	// k_xxh32_rows wave per SIMD (no LDS): both chains are latency-bound,
+	// so the checksums ride in k_index's idle issue slots
+	SideStream* side = nullptr;
+	hipError_t err = side_stream(side);
+	if (err != hipSuccess)
+		return err;
+	void* tab = nullptr;
+	err = hipMallocAsync(&tab, index_table_bytes(frame_len, nblocks), stream);
+	if (err != hipSuccess)
+		return err;
+	err = hipEventRecord(side->fork, stream);
+	if (err == hipSuccess)
+		err = hipStreamWaitEvent(side->s, side->fork, 0);
+	if (err == hipSuccess)
+		err = launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab), d_status,
+		                   stream);
+	if (err == hipSuccess)
+		err = launch_block_checksums(d_frame, d_desc, nblocks, d_status, side->s);
+	if (err == hipSuccess)
+		err = hipEventRecord(side->join, side->s);
+	if (err == hipSuccess)
+		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
+		                            static_cast<const uint8_t*>(tab), d_out, d_status, 0, stream);
+	if (err == hipSuccess)
+		err = launch_decode_pc(d_frame, frame_len, d_desc, nblocks, d_out, d_status, 1, 0, stream);
+	const hipError_t e2 = hipFreeAsync(tab, stream);
+	const hipError_t e3 = hipStreamWaitEvent(stream, side->join, 0);
+	return err != hipSuccess ? err : (e2 != hipSuccess ? e2 : e3);
 }
 
 hipError_t launch_block_checksums(const uint8_t* d_frame, const lz4ada_block_desc* d_desc,
@@ -2087,8 +2323,8 @@ hipError_t launch_block_checksums(const uint8_t* d_frame, const lz4ada_block_des
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	hipLaunchKernelGGL(k_block_checksums, dim3(nblocks), dim3(64), 0, stream, d_frame, d_desc,
-	                   nblocks, d_status);
+	hipLaunchKernelGGL(k_xxh32_rows, dim3((nblocks + XG - 1) / XG), dim3(64), 0, stream, d_frame,
+	                   (const uint8_t*)nullptr, d_desc, nblocks, d_status, (uint32_t*)nullptr);
 	return hipGetLastError();
 }
 
@@ -2098,8 +2334,9 @@ hipError_t launch_output_checksums(const uint8_t* d_out, const lz4ada_block_desc
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	hipLaunchKernelGGL(k_output_checksums, dim3(nblocks), dim3(64), 0, stream, d_out, d_desc,
-	                   nblocks, d_status, d_hash);
+	hipLaunchKernelGGL(k_xxh32_rows, dim3((nblocks + XG - 1) / XG), dim3(64), 0, stream,
+	                   (const uint8_t*)nullptr, d_out, d_desc, nblocks,
+	                   const_cast<lz4ada_block_status*>(d_status), d_hash);
 	return hipGetLastError();
 }
 

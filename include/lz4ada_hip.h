@@ -208,7 +208,10 @@ int lz4ada_frame_index(const uint8_t *frame, int64_t len, lz4ada_frame_info *inf
 
 /* Launch the per-block kernels over a device-resident frame: block XXH32
  * (when LZ4ADA_BLOCK_HAS_CKSUM) and decode into d_out.  Asynchronous on
- * `stream` (hipStream_t).  d_frame must stay readable up to frame_len. */
+ * `stream` (hipStream_t).  d_frame must stay readable up to frame_len.
+ * The checksums run on a library-owned side stream beside the decoder's
+ * first pass (forked from and joined back into `stream` by events; set
+ * LZ4ADA_NO_OVERLAP to serialise them). */
 int lz4ada_decode_blocks_device(const void *d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc *d_descs, int64_t nblocks,
                                 void *d_out, lz4ada_block_status *d_status,

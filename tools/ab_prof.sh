@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-kernel A/B: rocprofv3 --kernel-trace --stats of tools/time_decode.py for
 # the product and every bo-lz4-ada_amd/_variants/*.so; prints the average
-# duration of each decode kernel.  Usage (GPU box): bash tools/ab_prof.sh [kinds]
+# duration of each decode kernel.  Usage (GPU box): [EXTRA=--checksums] bash tools/ab_prof.sh [kinds]
 KINDS=${1:-"mixed dense"}
 shopt -s nullglob
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
@@ -11,7 +11,7 @@ for k in $KINDS; do
     out=gpurun_out/abp/${name}_$k
     mkdir -p $out
     LZ4ADA_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o run \
-      -- python3 tools/time_decode.py --kind $k > $out/log 2>&1 || exit 1
+      -- python3 tools/time_decode.py --kind $k $EXTRA > $out/log 2>&1 || exit 1
     python3 - "$out" "$name" "$k" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]

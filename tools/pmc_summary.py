@@ -24,7 +24,7 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = ("k_decode_idx", "k_index", "k_decode_pc", "k_decode_wg", "k_decode_blocks",
-           "k_block_checksums", "k_output_checksums", "k_serial_block", "k_xxh32_update",
+           "k_xxh32_rows", "k_serial_block", "k_xxh32_update",
            "k_compact")
 
 

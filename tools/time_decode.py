@@ -26,18 +26,35 @@ def main():
     ap.add_argument("--kind", default="mixed")
     ap.add_argument("--blocks", type=int, default=2048)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--checksums", action="store_true",
+                    help="also run the block and output XXH32 kernels each step (and check them once)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     bmax = 4 << 20
     recs = bench.make_unique_blocks(lz4ada.GEN_KINDS[args.kind], 64, bmax)
-    d_frame, frame_len, d_desc, _, comp, raw, _ = bench.build_shard(recs, 0, args.blocks, bmax, dev)
+    d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = bench.build_shard(recs, 0, args.blocks,
+                                                                                bmax, dev)
     d_out = torch.empty(args.blocks * bmax, dtype=torch.uint8, device=dev)
     d_status = torch.zeros(args.blocks * 32, dtype=torch.uint8, device=dev)
     sh = torch.cuda.current_stream(dev).cuda_stream
-    launch = lambda: lz4ada.launch_decode(d_frame.data_ptr(), frame_len, d_desc.data_ptr(), args.blocks,
-                                          d_out.data_ptr(), d_status.data_ptr(), sh)
+    d_hash = torch.zeros(args.blocks, dtype=torch.int32, device=dev)
+
+    def launch():
+        if args.checksums:
+            lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), args.blocks,
+                                          d_status.data_ptr(), sh)
+        lz4ada.launch_decode(d_frame.data_ptr(), frame_len, d_desc.data_ptr(), args.blocks,
+                             d_out.data_ptr(), d_status.data_ptr(), sh)
+        if args.checksums:
+            lz4ada.output_checksums_device(d_out.data_ptr(), d_desc.data_ptr(), d_status.data_ptr(),
+                                           args.blocks, d_hash.data_ptr(), sh)
+
     launch()
     torch.cuda.synchronize()
+    if args.checksums:
+        st = bench.check_statuses(d_status, args.blocks)
+        assert all(s.cksum == d.cksum for s, d in zip(st, descs)), "block checksum mismatch"
+        assert [h & 0xffffffff for h in d_hash.cpu().tolist()] == exp_hash, "output hash mismatch"
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.steps):
