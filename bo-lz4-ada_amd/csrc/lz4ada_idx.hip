@@ -46,6 +46,14 @@ constexpr int BATCH = 64 * SUB;     // pass-2 batch (2 KiB of input)
 constexpr int RING = 4 * BATCH;     // pass-2 staging ring
 constexpr int LONG = 256;           // runs longer than this are copied by the whole wave
 constexpr int32_t MAX_RUN = 1 << 28;  // length guard (block_max <= 4 MiB in the bulk path)
+// Pass-1 lead-in (k_index): each lane first walks from this many bytes
+// before its segment: about LEAD_SEQ sequences at the previous chunk's
+// density (the first chunk: LEAD_IN0 bytes).
+#ifndef LZ4ADA_LEAD_SEQ
+#define LZ4ADA_LEAD_SEQ 45
+#endif
+constexpr int32_t LEAD_SEQ = LZ4ADA_LEAD_SEQ;
+constexpr int32_t LEAD_IN0 = 256, LEAD_MIN = 256, LEAD_MAX = 768;
 
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -53,7 +61,7 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::
 // waves (each stamp drains the wave's memory counters: read shares).
 enum IdxPhase { I_STAGE, I_WALK0, I_ITER, I_CHUNKS, I_ITERS,
 	            D_STAGE, D_WALK1, D_WALK2, D_TLDS, D_LIT, D_MFAR, D_NEAR, D_FLUSH, D_GLOBAL,
-	            D_BATCHES, D_GBATCHES, D_ROUNDS, D_TASKS, D_LANES, IDX_NST };
+	            D_BATCHES, D_GBATCHES, D_ROUNDS, D_TASKS, D_LANES, I_STEPS, I_MAXST, IDX_NST };
 #ifdef LZ4ADA_IDX_STAMPS
 __device__ unsigned long long g_idx_stamps[IDX_NST];
 #define ISTAMP_DECL uint64_t ist[IDX_NST] = {}; uint64_t ist_t = __builtin_amdgcn_s_memtime()
@@ -329,8 +337,9 @@ struct alignas(16) IdxLds {
 __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t s, int32_t seg_end,
                                                 int32_t n, uint32_t* rb, uint16_t* rc, uint32_t* ghi,
                                                 bool& err, int32_t& epos, int32_t y_old,
-                                                bool may_stop)
+                                                bool may_stop, int32_t& nst)
 {
+	nst = 0;  // sequence steps (diagnostic counts; dead in the product)
 	err = false;
 	epos = INT32_MAX;
 	auto put = [&](int32_t k, uint32_t b, uint32_t c) {
@@ -361,6 +370,7 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 		if (may_stop && (rb[k] & bit))
 			merged = true;  // rb[k] is still the previous walk's record
 		bm |= bit;
+		++nst;
 		Seq q;
 		if (!parse_fast(S, p, n, q)) {
 			err = true;
@@ -376,6 +386,12 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 		for (; nxt < NSUB; ++nxt)
 			put(nxt, 0, 0);
 	return p;
+}
+
+__device__ __forceinline__ int32_t lead_in_bytes(int32_t starts)
+{
+	const int32_t l = LEAD_SEQ * (CHUNK / max(starts, 1));
+	return __builtin_amdgcn_readfirstlane(min(max(l, LEAD_MIN), LEAD_MAX));
 }
 
 // Inclusive prefix maximum over the wave (values >= 0), DPP as wave_incl_scan.
@@ -439,6 +455,7 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 
 	ISTAMP_DECL;
 	int32_t E = 0;  // exact chain entry of the current chunk
+	int32_t lead = LEAD_IN0;  // lead-in bytes (from the previous chunk's density)
 	bool bad = false;
 	for (int32_t C = 0; C < n && !bad; C += CHUNK) {
 		// stage block-relative [C - mis, C - mis + CHUNK) (16-byte aligned addresses)
@@ -462,6 +479,22 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 		// the true chain, and a run of segments a long sequence jumps over
 		// is crossed in one step instead of one iteration per segment.
 		int32_t ein = (lane == 0) ? E : s;
+		if (lane > 0 && s < n) {
+			// Lead-in: walk from OV bytes before the segment to find a
+			// likelier entry than s itself -- chains from a wrong start merge
+			// with the true one within ~14 sequences, so by s this one mostly
+			// has, and the re-walk rounds below (most of pass 1's time) are
+			// rarely needed.  A malformed lead-in keeps s.
+			int32_t p = max(s - lead, C);  // inside the staged chunk
+			bool ok = true;
+			while (ok && p < s) {
+				Seq q;
+				ok = parse_fast(S, p, n, q);
+				p = q.next;
+			}
+			if (ok)
+				ein = p;
+		}
 		uint32_t* ghi = reinterpret_cast<uint32_t*>(tab + (C >> 5) + NSUB * lane) + 1;
 #ifdef LZ4ADA_IDX_NO_MERGE_STOP
 		constexpr bool no_stop = true;
@@ -470,10 +503,13 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 #endif
 		int32_t epos = INT32_MAX;
 		bool err = false;
+		int32_t nst = 0;
 		int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, err,
-		                                   epos, 0, false)
+		                                   epos, 0, false, nst)
 		                    : ein;
 		ISTAMP(I_WALK0);
+		ICOUNT(I_STEPS, __shfl(wave_incl_scan(nst), 63));
+		ICOUNT(I_MAXST, __shfl(wave_incl_max(nst), 63));
 		for (int it = 0; it < 64; ++it) {
 			int32_t prev = __shfl_up(wave_incl_max(y), 1);
 			if (lane == 0)
@@ -482,16 +518,19 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			if (!__any(changed))
 				break;
 			ICOUNT(I_ITERS, 1);
+			nst = 0;
 			if (changed) {
 				ein = prev;
 				if (s < n) {
 					y = walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, err, epos, y,
-					                 !err && !no_stop);
+					                 !err && !no_stop, nst);
 				} else {
 					y = ein;
 					err = false;
 				}
 			}
+			ICOUNT(I_STEPS, __shfl(wave_incl_scan(nst), 63));
+			ICOUNT(I_MAXST, __shfl(wave_incl_max(nst), 63));
 		}
 		ISTAMP(I_ITER);
 		// converged: every entry is the true chain position, and every
@@ -500,11 +539,13 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			bad = true;
 		bad = __any(bad);
 		wave_lds_fence();
+		int32_t starts = 0;  // sequence starts in this chunk (sizes the next lead-in)
 #pragma unroll
 		for (int i = 0; i < NSUB; ++i) {
 			const int32_t r = 64 * i + lane, sg = r / NSUB, sb = r & (NSUB - 1);
 			if (C + SEG * sg < n) {
 				const uint32_t bmv = X.rbm[sg][sb], c16 = X.rcnt[sg][sb];
+				starts += __popc(bmv);
 				if (c16 != 0xFFFFu)
 					tab[(C >> 5) + r] = uint64_t(bmv) | (uint64_t(c16) << 32);
 				else  // the exact count is in the high word already
@@ -512,6 +553,7 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			}
 		}
 		E = __shfl(wave_incl_max(y), 63);
+		lead = lead_in_bytes(__shfl(wave_incl_scan(starts), 63));
 		if (C == 0 && n >= 4 * CHUNK) {
 			// Sparse chains (over 64 input bytes per sequence: long literal
 			// runs) defeat the speculative walks -- every segment's guess

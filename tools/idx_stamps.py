@@ -21,8 +21,9 @@ import lz4ada  # noqa: E402
 
 NAMES = ["I_STAGE", "I_WALK0", "I_ITER", "I_CHUNKS", "I_ITERS",
          "D_STAGE", "D_WALK1", "D_WALK2", "D_TLDS", "D_LIT", "D_MFAR", "D_NEAR", "D_FLUSH", "D_GLOBAL",
-         "D_BATCHES", "D_GBATCHES", "D_ROUNDS", "D_TASKS", "D_LANES"]
-COUNTS = {"I_CHUNKS", "I_ITERS", "D_BATCHES", "D_GBATCHES", "D_ROUNDS", "D_TASKS", "D_LANES"}
+         "D_BATCHES", "D_GBATCHES", "D_ROUNDS", "D_TASKS", "D_LANES", "I_STEPS", "I_MAXST"]
+COUNTS = {"I_CHUNKS", "I_ITERS", "D_BATCHES", "D_GBATCHES", "D_ROUNDS", "D_TASKS", "D_LANES",
+          "I_STEPS", "I_MAXST"}
 
 
 def main():
