@@ -53,7 +53,10 @@ constexpr int32_t MAX_RUN = 1 << 28;  // length guard (block_max <= 4 MiB in the
 #define LZ4ADA_LEAD_SEQ 45
 #endif
 constexpr int32_t LEAD_SEQ = LZ4ADA_LEAD_SEQ;
-constexpr int32_t LEAD_IN0 = 256, LEAD_MIN = 256, LEAD_MAX = 768;
+#ifndef LZ4ADA_LEAD_MAX
+#define LZ4ADA_LEAD_MAX 768
+#endif
+constexpr int32_t LEAD_IN0 = 256, LEAD_MIN = 256, LEAD_MAX = LZ4ADA_LEAD_MAX;
 
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -388,6 +391,21 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 	return p;
 }
 
+// The chain position after the sequence at p, for the lead-in walk: only
+// a guess, so no checks, and every length extension taken as one byte (a
+// longer one just makes a wrong guess, which the re-walks fix) -- then the
+// token's dword pair is the one LDS read the step waits for.
+__device__ __forceinline__ int32_t skip_seq(const Src& S, int32_t p)
+{
+	const uint32_t a = uint32_t(p + S.mis) & S.mask;
+	const uint32_t* wa = reinterpret_cast<const uint32_t*>(S.lds + (a & ~3u));
+	const uint32_t w = __builtin_amdgcn_alignbyte(wa[1], wa[0], a & 3u);
+	const uint32_t tk = w & 0xffu;
+	const int32_t x1 = tk >= 0xf0u ? 1 : 0;
+	const int32_t L = int32_t(tk >> 4) + (x1 ? int32_t((w >> 8) & 0xffu) : 0);
+	return p + 3 + x1 + L + ((tk & 15u) == 15u ? 1 : 0);
+}
+
 __device__ __forceinline__ int32_t lead_in_bytes(int32_t starts)
 {
 	const int32_t l = LEAD_SEQ * (CHUNK / max(starts, 1));
@@ -484,16 +502,11 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 			// likelier entry than s itself -- chains from a wrong start merge
 			// with the true one within ~14 sequences, so by s this one mostly
 			// has, and the re-walk rounds below (most of pass 1's time) are
-			// rarely needed.  A malformed lead-in keeps s.
+			// rarely needed.
 			int32_t p = max(s - lead, C);  // inside the staged chunk
-			bool ok = true;
-			while (ok && p < s) {
-				Seq q;
-				ok = parse_fast(S, p, n, q);
-				p = q.next;
-			}
-			if (ok)
-				ein = p;
+			while (p < s)
+				p = skip_seq(S, p);
+			ein = p;
 		}
 		uint32_t* ghi = reinterpret_cast<uint32_t*>(tab + (C >> 5) + NSUB * lane) + 1;
 #ifdef LZ4ADA_IDX_NO_MERGE_STOP
@@ -1352,7 +1365,11 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #pragma unroll
 					for (int c = 0; c < GC; ++c)
 						if (g && 16 * c < rml[r])
+#ifdef LZ4ADA_IDX_EXP_NOVG  // timing experiment: no HBM match loads (wrong output)
+							vg[r][c] = u32x4{uint32_t(src), 0u, 0u, 0u};
+#else
 							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
+#endif
 					const int32_t nc = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
 					if (__any(nc > 0)) {
 						const int32_t inc = wave_incl_scan(nc);
@@ -1371,7 +1388,11 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 						if (lane < rtot[r]) {
 							rpd[r] = od + 16 * k;
 							rpn[r] = min(16, oml - 16 * k);
+#ifdef LZ4ADA_IDX_EXP_NOVG
+							vr[r] = u32x4{uint32_t(osrc), 0u, 0u, 0u};
+#else
 							__builtin_memcpy(&vr[r], ob + osrc + 16 * k, 16);
+#endif
 						}
 						wave_lds_fence();  // own[] is dealt again next round
 					}
