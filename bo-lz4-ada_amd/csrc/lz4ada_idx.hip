@@ -50,11 +50,11 @@ constexpr int32_t MAX_RUN = 1 << 28;  // length guard (block_max <= 4 MiB in the
 // before its segment: about LEAD_SEQ sequences at the previous chunk's
 // density (the first chunk: LEAD_IN0 bytes).
 #ifndef LZ4ADA_LEAD_SEQ
-#define LZ4ADA_LEAD_SEQ 45
+#define LZ4ADA_LEAD_SEQ 60
 #endif
 constexpr int32_t LEAD_SEQ = LZ4ADA_LEAD_SEQ;
 #ifndef LZ4ADA_LEAD_MAX
-#define LZ4ADA_LEAD_MAX 768
+#define LZ4ADA_LEAD_MAX 1024
 #endif
 constexpr int32_t LEAD_IN0 = 256, LEAD_MIN = 256, LEAD_MAX = LZ4ADA_LEAD_MAX;
 
