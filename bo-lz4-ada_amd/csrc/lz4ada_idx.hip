@@ -865,8 +865,13 @@ __device__ __forceinline__ void make_pattern16(uint64_t s0, uint64_t s1, int32_t
 	uint64_t x, hi;
 	if (off <= 8) {
 		x = off == 8 ? s0 : (s0 & ((uint64_t(1) << (8 * off)) - 1));
-		for (int32_t w = off; w < 8; w <<= 1)
-			x |= x << (8 * w);
+		// doubling x |= x << 8w for w = off, 2 off, 4 off while w < 8, with
+		// selects instead of a lane-divergent loop
+#pragma unroll
+		for (int i = 0; i < 3; ++i) {
+			const int32_t w = off << i;
+			x |= w < 8 ? x << (8 * w) : 0;
+		}
 		const uint32_t sh = uint32_t(off - 1);
 		stp = int32_t((PAT_LUT >> (5 * sh)) & 31u);
 		const int32_t r = int32_t((PAT_LUT >> (40 + 2 * sh)) & 3u);
@@ -982,8 +987,9 @@ __device__ __forceinline__ int32_t chunk_owner(DecLds& D, int32_t inc, int32_t n
 // is source byte i mod off, so a piece never reads its own match's output).
 // Pieces are in output order; one reading output of a lower lane of its
 // chunk waits until that lane has stored (ballot per step).
-__device__ __forceinline__ void ring_pieces(DecLds& D, int32_t mdst, int32_t off, int32_t ml)
+__device__ __forceinline__ int32_t ring_pieces(DecLds& D, int32_t mdst, int32_t off, int32_t ml)
 {
+	int32_t steps = 0;  // store steps (diagnostic count)
 	const int32_t lane = int32_t(lane_id());
 	const bool pat = off < 16 && off < ml;
 	const int32_t stp = pat ? pattern_step(off) : 16;
@@ -1030,27 +1036,28 @@ __device__ __forceinline__ void ring_pieces(DecLds& D, int32_t mdst, int32_t off
 				break;
 			const bool ready = pend && (dep & pm) == 0;
 			if (ready) {
-				u32x4 v;
+				// one load for every form (divergent per-form loads made a
+				// step run up to three of them one after the other)
+				int32_t rem = 0;
+				if (wide)
+					div_small(16 * k, ooff, rem);
+				const int32_t a1 = opat ? od - ooff : (wide ? od - ooff + rem : s_lo);
+				u32x4 v = oload16(D, a1);
+				if (wide && ooff - rem < 16)
+					v = merge_at(v, oload16(D, a1 - ooff), ooff - rem);
 				if (opat) {
-					v = oload16(D, od - ooff);
 					int32_t sstp;
 					make_pattern16(uint64_t(v.x) | (uint64_t(v.y) << 32),
 					               uint64_t(v.z) | (uint64_t(v.w) << 32), ooff, v, sstp);
-				} else if (wide) {
-					int32_t rem;
-					div_small(16 * k, ooff, rem);
-					v = oload16(D, od - ooff + rem);
-					if (ooff - rem < 16)
-						v = merge_at(v, oload16(D, od - ooff + rem - ooff), ooff - rem);
-				} else {
-					v = oload16(D, s_lo);
 				}
 				ostore(D, pd, v, pn);
 			}
 			pend = pend && !ready;
 			wave_lds_fence();
+			++steps;
 		}
 	}
+	return steps;
 }
 
 // Ring-sourced matches of a round of short matches, one lane each: those
@@ -1060,8 +1067,11 @@ __device__ __forceinline__ void ring_pieces(DecLds& D, int32_t mdst, int32_t off
 // searches over the round's monotone match positions, one AND against a
 // ballot per step).  rbeg: the round's first output position; L: this
 // lane's literal length.
-constexpr int RING_LANE_MAX = 32;
-__device__ __forceinline__ void ring_lanes(DecLds& D, int32_t mdst, int32_t off, int32_t ml,
+#ifndef LZ4ADA_RING_LANE_MAX
+#define LZ4ADA_RING_LANE_MAX 32
+#endif
+constexpr int RING_LANE_MAX = LZ4ADA_RING_LANE_MAX;
+__device__ __forceinline__ int32_t ring_lanes(DecLds& D, int32_t mdst, int32_t off, int32_t ml,
                                            int32_t rbeg, int32_t L)
 {
 	const int32_t lane = int32_t(lane_id());
@@ -1069,11 +1079,12 @@ __device__ __forceinline__ void ring_lanes(DecLds& D, int32_t mdst, int32_t off,
 	const int32_t dep_end = src + min(off, ml);
 	const bool far = ml > 0 && (dep_end <= rbeg || off <= L);
 	bool near = ml > 0 && !far;
+	int32_t steps = 0;  // near-match steps (diagnostic count)
 	if (far)
 		ring_match(D, mdst, off, ml);
 	wave_lds_fence();
 	if (!__any(near))
-		return;
+		return 0;
 	const int32_t mend = mdst + ml;
 	int32_t j1 = 0, c2 = 0;
 #pragma unroll
@@ -1097,7 +1108,9 @@ __device__ __forceinline__ void ring_lanes(DecLds& D, int32_t mdst, int32_t off,
 			near = false;
 		}
 		wave_lds_fence();
+		++steps;
 	}
+	return steps;
 }
 
 // Owner of piece t when lane i holds pieces [inc_i - cnt_i, inc_i) (inc: the
@@ -1247,7 +1260,6 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		const bool fit = incl <= OW && incl_s <= MAXSEQ;
 		const int32_t m = __popcll(__ballot(fit));  // lanes [0, m) form an LDS batch
 		ISTAMP(D_WALK1);
-		ICOUNT(D_LANES, m);
 
 		if (m == 0) {
 			// oversized: all 64 sub-segments straight to HBM
@@ -1539,6 +1551,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			if (64 * r < N) {
 				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
 				const bool hbm = ml > 0 && mdst - off < glo;
+#ifndef LZ4ADA_IDX_EXP_NOHBMST  // timing experiment (wrong output): no HBM-sourced stores
 				if (hbm) {
 #pragma unroll
 					for (int c = 0; c < GC; ++c)
@@ -1549,6 +1562,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				// 64 of the round were loaded in P, dealt over the wave
 				if (rpn[r] > 0)
 					ostore(D, rpd[r], vr[r], rpn[r]);
+#endif
 				if (rtot[r] > 64) {  // rare: deal the rest now
 					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;
 					const int32_t inc = wave_incl_scan(nc);
@@ -1572,10 +1586,19 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				// (every match at most RING_LANE_MAX bytes, e.g. dense data)
 				// keeps one lane per match -- the dealing's fixed cost
 				// (owner search, dependency masks) would dominate there
-				if (__any(rml_ring > RING_LANE_MAX))
-					ring_pieces(D, mdst, off, rml_ring);
-				else
-					ring_lanes(D, mdst, off, rml_ring, rbeg[r], rL[r]);
+#ifndef LZ4ADA_IDX_EXP_NORING  // timing experiment (wrong output): no ring-sourced matches
+				if (__any(rml_ring > RING_LANE_MAX)) {
+					const int32_t st = ring_pieces(D, mdst, off, rml_ring);
+					ICOUNT(D_TASKS, 1);
+					ICOUNT(D_ROUNDS, st);
+					(void)st;
+				} else {
+					const int32_t st = ring_lanes(D, mdst, off, rml_ring, rbeg[r], rL[r]);
+					ICOUNT(D_GBATCHES, 1);
+					ICOUNT(D_LANES, st);
+					(void)st;
+				}
+#endif
 			}
 		}
 #endif
