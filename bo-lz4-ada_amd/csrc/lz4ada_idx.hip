@@ -1000,7 +1000,11 @@ __device__ __forceinline__ int32_t ring_pieces(DecLds& D, int32_t mdst, int32_t 
 	for (int32_t t0 = 0; t0 < tot; t0 += 64) {
 		const int32_t t = t0 + lane;
 		const bool act = t < tot;
+#ifdef LZ4ADA_IDX_EXP_NOOWNER  // timing experiment (wrong output): no owner search
+		const int32_t lo = lane;
+#else
 		const int32_t lo = min(chunk_owner(D, inc, np, t0), 63);
+#endif
 		const int32_t k = t - (__shfl(inc, lo) - __shfl(np, lo));
 		const int32_t od = __shfl(mdst, lo), ooff = __shfl(off, lo), oml = __shfl(ml, lo);
 		const int32_t ostp = __shfl(stp, lo);
@@ -1016,7 +1020,11 @@ __device__ __forceinline__ int32_t ring_pieces(DecLds& D, int32_t mdst, int32_t 
 		// when every source ends before the chunk's first piece
 		const int32_t pe = act ? pd + 16 : INT32_MAX, ps = act ? pd : INT32_MAX;
 		uint64_t dep = 0;
+#ifdef LZ4ADA_IDX_EXP_NODEP  // timing experiment (wrong output): no dependency order
+		if (false) {
+#else
 		if (!__all(!act || s_hi <= __shfl(ps, 0))) {
+#endif
 			int32_t j1 = 0, c2 = 0;
 #pragma unroll
 			for (int st = 32; st >= 1; st >>= 1) {
