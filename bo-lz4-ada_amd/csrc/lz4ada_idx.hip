@@ -819,6 +819,7 @@ struct alignas(16) DecLds {
 	uint16_t cst[MAXSEQ];         // the batch's sequence starts, in order
 	uint8_t own[256];             // piece -> owning lane (dealt HBM pieces)
 	uint64_t rrec[4 * 64];        // pass-1 records of the staged chunks' sub-segments
+	uint64_t ldesc[2 * 64];       // literal runs of both rounds (dealt literal pieces)
 };
 
 // Exact-length store of n (1..16) bytes at output position x into the ring.
@@ -975,6 +976,25 @@ __device__ __forceinline__ int32_t chunk_owner(DecLds& D, int32_t inc, int32_t n
 	const int32_t excl = inc - np;
 	if (np > 0 && excl >= t0 && excl < t0 + 64)
 		D.own[excl - t0] = uint8_t(lane);
+	wave_lds_fence();
+	const int32_t v = D.own[lane];
+	wave_lds_fence();  // own[] is marked again for the next chunk
+	return wave_incl_max(v);
+}
+
+// chunk_owner over two rounds' entries (round 0's lanes, then round 1's:
+// entry 64 r + lane holds pieces [inc_r - np_r, inc_r)), owner 0..127.
+__device__ __forceinline__ int32_t chunk_owner2(DecLds& D, int32_t inc0, int32_t np0, int32_t inc1,
+                                                int32_t np1, int32_t t0)
+{
+	const int32_t lane = int32_t(lane_id());
+	const int32_t seed = __popcll(__ballot(inc0 <= t0)) + __popcll(__ballot(inc1 <= t0));
+	D.own[lane] = uint8_t(lane == 0 ? seed : 0);
+	const int32_t e0 = inc0 - np0, e1 = inc1 - np1;
+	if (np0 > 0 && e0 >= t0 && e0 < t0 + 64)
+		D.own[e0 - t0] = uint8_t(lane);
+	if (np1 > 0 && e1 >= t0 && e1 < t0 + 64)
+		D.own[e1 - t0] = uint8_t(64 + lane);
 	wave_lds_fence();
 	const int32_t v = D.own[lane];
 	wave_lds_fence();  // own[] is marked again for the next chunk
@@ -1422,35 +1442,45 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		ISTAMP(D_TLDS);
 
 		// L: literals (input ring -> output ring).  Short runs lane by lane;
-		// a round with a run over 32 bytes deals its 16-byte pieces over the
-		// whole wave instead.  (Storing a short last piece as 16 bytes that
+		// when a run is over 32 bytes, the 16-byte pieces of both rounds
+		// are dealt over the wave together (one chunk of 64 pieces fewer
+		// per batch than round by round), each piece reading its run from
+		// an LDS descriptor.  (Storing a short last piece as 16 bytes that
 		// spill into its own match, rewritten in M, measured no faster.)
+#ifndef LZ4ADA_IDX_EXP_NOLIT
+		static_assert(RMAX == 2, "literal dealing pairs two rounds");
+		{
+			const int32_t nc0 = (rL[0] + 15) >> 4, nc1 = (rL[1] + 15) >> 4;  // rL = 0: no sequence
+			if (__any(nc0 > 2 || nc1 > 2)) {
+				const int32_t inc0 = wave_incl_scan(nc0);
+				const int32_t tot0 = __shfl(inc0, 63);
+				const int32_t inc1 = tot0 + wave_incl_scan(nc1);
+				const int32_t tot = __shfl(inc1, 63);
+				auto pack = [&](int32_t lit, int32_t dst, int32_t L, int32_t excl) -> uint64_t {
+					return uint64_t(uint16_t(lit - base)) | (uint64_t(uint16_t(dst - o_batch)) << 16) |
+					       (uint64_t(uint16_t(L)) << 32) | (uint64_t(uint16_t(excl)) << 48);
+				};
+				D.ldesc[lane] = pack(rlit[0], rdst[0], rL[0], inc0 - nc0);
+				D.ldesc[64 + lane] = pack(rlit[1], rdst[1], rL[1], inc1 - nc1);
+				for (int32_t t0 = 0; t0 < tot; t0 += 64) {
+					const int32_t t = t0 + lane;
+					const int32_t lo = min(chunk_owner2(D, inc0, nc0, inc1, nc1, t0), 127);
+					const uint64_t dd = D.ldesc[lo];
+					const int32_t lit = base + int32_t(dd & 0xffffu);
+					const int32_t dst = o_batch + int32_t((dd >> 16) & 0xffffu);
+					const int32_t L = int32_t((dd >> 32) & 0xffffu);
+					const int32_t k = t - int32_t(dd >> 48);
+					if (t < tot)
+						ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, L - 16 * k));
+				}
+			} else {
 #pragma unroll
-		for (int r = 0; r < RMAX; ++r) {
-			if (64 * r < N) {
-#ifdef LZ4ADA_IDX_EXP_NOLIT
-				if (1) continue;
-#endif
-				const int32_t nc = (rL[r] + 15) >> 4;
-				if (__any(nc > 2)) {
-					const int32_t inc = wave_incl_scan(nc);
-					const int32_t tot = __shfl(inc, 63);
-					for (int32_t t0 = 0; t0 < tot; t0 += 64) {
-						const int32_t t = t0 + lane;
-						const int32_t lo = min(chunk_owner(D, inc, nc, t0), 63);
-						const int32_t k = t - (__shfl(inc, lo) - __shfl(nc, lo));
-						const int32_t L = __shfl(rL[r], lo);
-						const int32_t lit = __shfl(rlit[r], lo);
-						const int32_t dst = __shfl(rdst[r], lo);
-						if (t < tot)
-							ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, L - 16 * k));
-					}
-				} else {
+				for (int r = 0; r < RMAX; ++r)
 					for (int32_t c = 0; c < rL[r]; c += 16)
 						ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), min(16, rL[r] - c));
-				}
 			}
 		}
+#endif
 		wave_lds_fence();
 		ISTAMP(D_LIT);
 
