@@ -1007,28 +1007,53 @@ __device__ __forceinline__ int32_t chunk_owner2(DecLds& D, int32_t inc0, int32_t
 // is source byte i mod off, so a piece never reads its own match's output).
 // Pieces are in output order; one reading output of a lower lane of its
 // chunk waits until that lane has stored (ballot per step).
-__device__ __forceinline__ int32_t ring_pieces(DecLds& D, int32_t mdst, int32_t off, int32_t ml)
+// Pieces of one match: 16-byte pieces, or stp-byte steps of a period-off
+// pattern (off < 16 < ml overlaps).
+__device__ __forceinline__ int32_t match_pieces(int32_t off, int32_t ml)
+{
+	if (ml <= 0)
+		return 0;
+	if (!(off < 16 && off < ml))
+		return (ml + 15) >> 4;
+	const int32_t stp = pattern_step(off);
+	int32_t rr;
+	return stp == 16 ? (ml + 15) >> 4 : div_small(ml + stp - 1, stp, rr);
+}
+
+// Both rounds' ring-sourced matches (round r: mdst[r], off[r], ml[r]; ml 0:
+// none), dealt together in output order; a piece finds its match in an LDS
+// descriptor (D.ldesc, free after the literals) instead of by shuffles.
+__device__ __forceinline__ int32_t ring_pieces(DecLds& D, const int32_t (&mdst)[RMAX],
+                                               const int32_t (&off)[RMAX], const int32_t (&ml)[RMAX],
+                                               int32_t o_batch)
 {
 	int32_t steps = 0;  // store steps (diagnostic count)
 	const int32_t lane = int32_t(lane_id());
-	const bool pat = off < 16 && off < ml;
-	const int32_t stp = pat ? pattern_step(off) : 16;
-	int32_t rr;
-	const int32_t np = ml <= 0 ? 0 : (stp == 16 ? (ml + 15) >> 4 : div_small(ml + stp - 1, stp, rr));
-	const int32_t inc = wave_incl_scan(np);
-	const int32_t tot = __shfl(inc, 63);
+	const int32_t np0 = match_pieces(off[0], ml[0]), np1 = match_pieces(off[1], ml[1]);
+	const int32_t inc0 = wave_incl_scan(np0);
+	const int32_t tot0 = __shfl(inc0, 63);
+	const int32_t inc1 = tot0 + wave_incl_scan(np1);
+	const int32_t tot = __shfl(inc1, 63);
+	auto pack = [&](int32_t md, int32_t of, int32_t m, int32_t excl) -> uint64_t {
+		return uint64_t(uint16_t(md - o_batch)) | (uint64_t(uint16_t(of)) << 16) |
+		       (uint64_t(uint16_t(m)) << 32) | (uint64_t(uint16_t(excl)) << 48);
+	};
+	D.ldesc[lane] = pack(mdst[0], off[0], ml[0], inc0 - np0);
+	D.ldesc[64 + lane] = pack(mdst[1], off[1], ml[1], inc1 - np1);
 	for (int32_t t0 = 0; t0 < tot; t0 += 64) {
 		const int32_t t = t0 + lane;
 		const bool act = t < tot;
 #ifdef LZ4ADA_IDX_EXP_NOOWNER  // timing experiment (wrong output): no owner search
 		const int32_t lo = lane;
 #else
-		const int32_t lo = min(chunk_owner(D, inc, np, t0), 63);
+		const int32_t lo = min(chunk_owner2(D, inc0, np0, inc1, np1, t0), 127);
 #endif
-		const int32_t k = t - (__shfl(inc, lo) - __shfl(np, lo));
-		const int32_t od = __shfl(mdst, lo), ooff = __shfl(off, lo), oml = __shfl(ml, lo);
-		const int32_t ostp = __shfl(stp, lo);
+		const uint64_t dd = D.ldesc[lo];
+		const int32_t od = o_batch + int32_t(dd & 0xffffu);
+		const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
+		const int32_t k = t - int32_t(dd >> 48);
 		const bool opat = ooff < 16 && ooff < oml;
+		const int32_t ostp = opat ? pattern_step(ooff) : 16;
 		const bool wide = !opat && oml > ooff;  // overlap with off >= 16
 		const int32_t pd = od + k * ostp;
 		const int32_t pn = min(16, oml - k * ostp);
@@ -1574,18 +1599,21 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			}
 		}
 #else
-		// M: matches, round by round in output order.  HBM-sourced matches
-		// store the pieces loaded in P.  Every match whose source is in the
-		// LDS ring -- before the round, in its own literals, or in this
-		// round's output (near) -- is cut into pieces dealt over the wave,
-		// 16 bytes each (a period-off pattern: stp bytes, so every piece
-		// starts at phase 0), so a round costs its piece count / 64, not
-		// its longest match.  A piece reading this chunk's output runs once
-		// every lower lane it reads from has stored (one AND against a
-		// ballot per step; pieces of one match never read each other: match
-		// byte i is source byte i mod off).
+		// M: matches.  HBM-sourced matches store the pieces loaded in P,
+		// both rounds first.  Every match whose source is in the LDS ring --
+		// before the batch, in its own literals, or in this batch's match
+		// output (near) -- is then cut into pieces dealt over the wave, both
+		// rounds together in output order, 16 bytes each (a period-off
+		// pattern: stp bytes, so every piece starts at phase 0), so a batch
+		// costs its piece count / 64, not its longest match.  A piece
+		// reading this chunk's output runs once every lower lane it reads
+		// from has stored (one AND against a ballot per step; pieces of one
+		// match never read each other: match byte i is source byte i mod
+		// off).
+		int32_t mring[RMAX], oring[RMAX], lring[RMAX];  // the rounds' ring-sourced matches
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
+			mring[r] = oring[r] = lring[r] = 0;
 			if (64 * r < N) {
 				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
 				const bool hbm = ml > 0 && mdst - off < glo;
@@ -1617,28 +1645,39 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 						}
 					}
 				}
-				wave_lds_fence();
-				ISTAMP(D_MFAR);
-				const int32_t rml_ring = (ml > 0 && !hbm) ? ml : 0;
-				// long ring matches: dealt pieces; a round of short ones
-				// (every match at most RING_LANE_MAX bytes, e.g. dense data)
-				// keeps one lane per match -- the dealing's fixed cost
-				// (owner search, dependency masks) would dominate there
+				mring[r] = mdst;
+				oring[r] = off;
+				lring[r] = (ml > 0 && !hbm) ? ml : 0;
+			}
+		}
+		// every HBM-sourced match of the batch is stored before the ring
+		// matches run (none reads another's output: their sources are in HBM)
+		wave_lds_fence();
+		ISTAMP(D_MFAR);
+		// ring-sourced matches: with a long one (over RING_LANE_MAX bytes) in
+		// the batch, the pieces of both rounds are dealt over the wave
+		// together; rounds of short ones only (e.g. dense data) keep one lane
+		// per match -- the dealing's fixed cost (owner search, dependency
+		// masks) would dominate there
 #ifndef LZ4ADA_IDX_EXP_NORING  // timing experiment (wrong output): no ring-sourced matches
-				if (__any(rml_ring > RING_LANE_MAX)) {
-					const int32_t st = ring_pieces(D, mdst, off, rml_ring);
-					ICOUNT(D_TASKS, 1);
-					ICOUNT(D_ROUNDS, st);
-					(void)st;
-				} else {
-					const int32_t st = ring_lanes(D, mdst, off, rml_ring, rbeg[r], rL[r]);
+		static_assert(RMAX == 2, "ring dealing pairs two rounds");
+		if (__any(lring[0] > RING_LANE_MAX || lring[1] > RING_LANE_MAX)) {
+			const int32_t st = ring_pieces(D, mring, oring, lring, o_batch);
+			ICOUNT(D_TASKS, 1);
+			ICOUNT(D_ROUNDS, st);
+			(void)st;
+		} else {
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				if (64 * r < N) {
+					const int32_t st = ring_lanes(D, mring[r], oring[r], lring[r], rbeg[r], rL[r]);
 					ICOUNT(D_GBATCHES, 1);
 					ICOUNT(D_LANES, st);
 					(void)st;
 				}
-#endif
 			}
 		}
+#endif
 #endif
 		ISTAMP(D_NEAR);
 
