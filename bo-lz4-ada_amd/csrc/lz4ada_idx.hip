@@ -1406,13 +1406,15 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 
 		// HBM-sourced matches: every load in flight before the first use.  A
 		// match's first GC pieces load in its own lane; the pieces beyond
-		// (long matches) are dealt over the wave, one per lane and round
-		// (more than 64 in a round: loaded in M, rare).
-		u32x4 vg[RMAX][GC], vr[RMAX];
-		int32_t rtot[RMAX], rpd[RMAX], rpn[RMAX];
+		// (long matches) of both rounds are dealt over the wave, one per
+		// lane, through the LDS match descriptors (more than 64: the rest
+		// load in M, rare).
+		u32x4 vg[RMAX][GC], vr = u32x4{0u, 0u, 0u, 0u};
+		int32_t rtot[RMAX], rfirst[RMAX];  // pieces beyond GC per round; the first not dealt here
+		int32_t rpd = 0, rpn = 0;          // this lane's dealt piece
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r)
-			rtot[r] = rpd[r] = rpn[r] = 0;
+			rtot[r] = rfirst[r] = 0;
 		if (__any(anyg)) {
 			// the previous batch's flush (FLUSH_ST store instructions) and
 			// the input and record prefetch (3 loads, when this batch
@@ -1422,8 +1424,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FLUSH_ST + 3) : "memory");
 			else
 				asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FLUSH_ST) : "memory");
+			int32_t nc[RMAX];
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
+				nc[r] = 0;
 				if (64 * r < N) {
 					const int32_t src = rdst[r] + rL[r] - roff[r];
 					const bool g = rml[r] > 0 && src < glo;
@@ -1435,33 +1439,40 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #else
 							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
 #endif
-					const int32_t nc = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
-					if (__any(nc > 0)) {
-						const int32_t inc = wave_incl_scan(nc);
-						const int32_t excl = inc - nc;
-						rtot[r] = __shfl(inc, 63);
-						for (int32_t k = 0; k < nc; ++k)
-							if (excl + k < 64)
-								D.own[excl + k] = uint8_t(lane);
-						wave_lds_fence();
-						// shuffles with every lane active (ds_bpermute does not
-						// read a lane the EXEC mask has switched off)
-						const int32_t o = D.own[lane] & 63;
-						const int32_t k = GC + lane - __shfl(excl, o);
-						const int32_t osrc = __shfl(src, o);
-						const int32_t od = __shfl(rdst[r] + rL[r], o), oml = __shfl(rml[r], o);
-						if (lane < rtot[r]) {
-							rpd[r] = od + 16 * k;
-							rpn[r] = min(16, oml - 16 * k);
-#ifdef LZ4ADA_IDX_EXP_NOVG
-							vr[r] = u32x4{uint32_t(osrc), 0u, 0u, 0u};
-#else
-							__builtin_memcpy(&vr[r], ob + osrc + 16 * k, 16);
-#endif
-						}
-						wave_lds_fence();  // own[] is dealt again next round
-					}
+					nc[r] = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
 				}
+			}
+			static_assert(RMAX == 2, "HBM piece dealing pairs two rounds");
+			if (__any(nc[0] > 0 || nc[1] > 0)) {
+				const int32_t inc0 = wave_incl_scan(nc[0]);
+				const int32_t tot0 = __shfl(inc0, 63);
+				const int32_t inc1 = tot0 + wave_incl_scan(nc[1]);
+				const int32_t tot = __shfl(inc1, 63);
+				rtot[0] = tot0;
+				rtot[1] = tot - tot0;
+				rfirst[0] = 64;
+				rfirst[1] = max(64 - tot0, 0);
+				auto pack = [&](int32_t md, int32_t of, int32_t m, int32_t excl) -> uint64_t {
+					return uint64_t(uint16_t(md - o_batch)) | (uint64_t(uint16_t(of)) << 16) |
+					       (uint64_t(uint16_t(m)) << 32) | (uint64_t(uint16_t(excl)) << 48);
+				};
+				D.ldesc[lane] = pack(rdst[0] + rL[0], roff[0], rml[0], inc0 - nc[0]);
+				D.ldesc[64 + lane] = pack(rdst[1] + rL[1], roff[1], rml[1], inc1 - nc[1]);
+				const int32_t lo = min(chunk_owner2(D, inc0, nc[0], inc1, nc[1], 0), 127);
+				const uint64_t dd = D.ldesc[lo];
+				const int32_t od = o_batch + int32_t(dd & 0xffffu);
+				const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
+				const int32_t k = GC + lane - int32_t(dd >> 48);
+				if (lane < tot) {
+					rpd = od + 16 * k;
+					rpn = min(16, oml - 16 * k);
+#ifdef LZ4ADA_IDX_EXP_NOVG
+					vr = u32x4{uint32_t(od - ooff), 0u, 0u, 0u};
+#else
+					__builtin_memcpy(&vr, ob + (od - ooff) + 16 * k, 16);
+#endif
+				}
+				wave_lds_fence();  // ldesc / own[] are written again later
 			}
 		}
 		ISTAMP(D_TLDS);
@@ -1509,96 +1520,6 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		wave_lds_fence();
 		ISTAMP(D_LIT);
 
-#ifdef LZ4ADA_IDX_OLD_M
-		// M: matches, round by round in output order.  Everything before the
-		// round is final, so a match whose (non-self) source ends there (or
-		// lies in its own literals) runs at once; a near match -- one reading
-		// this round's match output -- runs once every lane it reads from is
-		// done.
-#pragma unroll
-		for (int r = 0; r < RMAX; ++r) {
-			if (64 * r < N) {
-				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
-				const int32_t src = mdst - off;
-				const int32_t dep_end = src + min(off, ml);
-				// runs now: a source before the round, or inside this
-				// sequence's own literals (off <= L)
-				const bool far = ml > 0 && (dep_end <= rbeg[r] || off <= rL[r]);
-				bool near = ml > 0 && !far;
-				const bool hbm = far && src < glo;
-				if (far) {
-					if (hbm) {
-#ifndef LZ4ADA_IDX_EXP_NOHBMST
-#pragma unroll
-						for (int c = 0; c < GC; ++c)
-							if (16 * c < ml)
-								ostore(D, mdst + 16 * c, vg[r][c], min(16, ml - 16 * c));
-#endif
-					} else {
-#ifndef LZ4ADA_IDX_EXP_NORING
-						ring_match(D, mdst, off, ml);
-#endif
-					}
-				}
-				// pieces of HBM-sourced matches beyond the first GC: the first
-				// 64 of the round were loaded in P, dealt over the wave
-				if (rpn[r] > 0)
-					ostore(D, rpd[r], vr[r], rpn[r]);
-				if (rtot[r] > 64) {  // rare: deal the rest now
-					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;
-					const int32_t inc = wave_incl_scan(nc);
-					for (int32_t t0 = 64; t0 < rtot[r]; t0 += 64) {
-						const int32_t t = t0 + lane;
-						const int32_t lo = piece_owner(inc, t);
-						const int32_t k = GC + t - (__shfl(inc, lo) - __shfl(nc, lo));
-						const int32_t osrc = __shfl(src, lo), odst = __shfl(mdst, lo);
-						const int32_t oml = __shfl(ml, lo);
-						if (t < rtot[r]) {
-							u32x4 v;
-							__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
-							ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
-						}
-					}
-				}
-				wave_lds_fence();
-				ISTAMP(D_MFAR);
-#ifdef LZ4ADA_IDX_EXP_NONEAR
-				near = false;
-#endif
-				if (__any(near)) {
-					// lanes whose match output this near match reads: those
-					// with mend > src and mdst < dep_end (both monotone along
-					// the round, so two binary searches)
-					const int32_t mend = mdst + ml;
-					int32_t j1 = 0, c2 = 0;
-#pragma unroll
-					for (int st = 32; st >= 1; st >>= 1) {
-						if (__shfl(mend, j1 + st - 1) <= src)
-							j1 += st;
-						if (__shfl(mdst, c2 + st - 1) < dep_end)
-							c2 += st;
-					}
-					const int32_t j2 = min(c2 - 1, lane - 1);
-					uint64_t dep = 0;
-					if (near && j1 <= j2)
-						dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) &
-						      ~((uint64_t(1) << j1) - 1);
-					for (;;) {
-						const uint64_t pending = __ballot(near);
-						if (pending == 0)
-							break;
-						ICOUNT(D_ROUNDS, 1);
-						const bool ready = near && (dep & pending) == 0;
-						if (ready) {
-							ring_match(D, mdst, off, ml);
-							near = false;
-						}
-						wave_lds_fence();
-					}
-				}
-			}
-		}
-#else
 		// M: matches.  HBM-sourced matches store the pieces loaded in P,
 		// both rounds first.  Every match whose source is in the LDS ring --
 		// before the batch, in its own literals, or in this batch's match
@@ -1611,6 +1532,12 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		// match never read each other: match byte i is source byte i mod
 		// off).
 		int32_t mring[RMAX], oring[RMAX], lring[RMAX];  // the rounds' ring-sourced matches
+#ifndef LZ4ADA_IDX_EXP_NOHBMST
+		// pieces of HBM-sourced matches beyond the first GC, dealt and
+		// loaded in P (the first 64 of the batch)
+		if (rpn > 0)
+			ostore(D, rpd, vr, rpn);
+#endif
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
 			mring[r] = oring[r] = lring[r] = 0;
@@ -1624,15 +1551,11 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 						if (16 * c < ml)
 							ostore(D, mdst + 16 * c, vg[r][c], min(16, ml - 16 * c));
 				}
-				// pieces of HBM-sourced matches beyond the first GC: the first
-				// 64 of the round were loaded in P, dealt over the wave
-				if (rpn[r] > 0)
-					ostore(D, rpd[r], vr[r], rpn[r]);
 #endif
-				if (rtot[r] > 64) {  // rare: deal the rest now
+				if (rtot[r] > rfirst[r]) {  // rare: more than 64 dealt pieces; the rest now
 					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;
 					const int32_t inc = wave_incl_scan(nc);
-					for (int32_t t0 = 64; t0 < rtot[r]; t0 += 64) {
+					for (int32_t t0 = rfirst[r]; t0 < rtot[r]; t0 += 64) {
 						const int32_t t = t0 + lane;
 						const int32_t lo = piece_owner(inc, t);
 						const int32_t k = GC + t - (__shfl(inc, lo) - __shfl(nc, lo));
@@ -1677,7 +1600,6 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				}
 			}
 		}
-#endif
 #endif
 		ISTAMP(D_NEAR);
 
