@@ -58,7 +58,15 @@ constexpr int32_t LEAD_SEQ = LZ4ADA_LEAD_SEQ;
 #endif
 constexpr int32_t LEAD_IN0 = 256, LEAD_MIN = 256, LEAD_MAX = LZ4ADA_LEAD_MAX;
 
-__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// vmcnt(0) through the builtin, so the compiler's wait pass sees it (an asm
+// wait leaves the loads pending in its model: later register reuse on any
+// path merging with this one then waits again)
+__device__ __forceinline__ void vm_wait()
+{
+	asm volatile("" ::: "memory");
+	__builtin_amdgcn_s_waitcnt(0x0F70);
+	asm volatile("" ::: "memory");
+}
 
 // Diagnostic build only (-DLZ4ADA_IDX_STAMPS): cycles per phase, summed over
 // waves (each stamp drains the wave's memory counters: read shares).
@@ -1245,6 +1253,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			if (x + 16 * lane < 0)
 				*reinterpret_cast<u32x4*>(&D.oring[uint32_t(x + 16 * lane) & OMASK]) =
 				    gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(intptr_t(x + 16 * lane)), olim);
+		__builtin_amdgcn_s_waitcnt(0x0F70);  // settled before the batch loop (see fetch4)
 		wave_lds_fence();
 	}
 	const uint64_t* tab = reinterpret_cast<const uint64_t*>(tab_all) + (((d.in_off >> 8) + b) << 3);
@@ -1269,6 +1278,9 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		return k < nsub ? __builtin_nontemporal_load(tab + k) : 0;
 	};
 	uint64_t pr = load_rec(0);
+	// settled before the loop: left pending, the loop head's merge would
+	// make every batch's staging wait vmcnt(0) (flush stores included)
+	vm_wait();
 
 	ISTAMP_DECL;
 	int32_t o_batch = 0;  // output position of the current batch
@@ -1280,7 +1292,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		bool staged = false;
 		if (hi < cf + 3) {
 			staged = true;
-			while (hi < cf + 3) {
+			auto stage_one = [&]() {
 				const uint32_t a = uint32_t(hi * BATCH) & (RING - 1);
 				*reinterpret_cast<u32x4*>(&D.ring[a + 16 * lane]) = pf0;
 				*reinterpret_cast<u32x4*>(&D.ring[a + 1024 + 16 * lane]) = pf1;
@@ -1290,7 +1302,13 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				++hi;
 				load_chunk2(abase, hi, lim, pf0, pf1);
 				pr = load_rec(hi);
-			}
+			};
+			// the first chunk outside the loop: its prefetch is settled (M's
+			// wait), and inside a loop the wait pass would put a vmcnt(0) --
+			// the previous batch's flush stores included -- before it too
+			stage_one();
+			while (hi < cf + 3)  // the block's first batch (and rarely later)
+				stage_one();
 			wave_lds_fence();
 		}
 		S.lo = max(hi - 4, 0) * BATCH - mis;
@@ -1532,6 +1550,11 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		// match never read each other: match byte i is source byte i mod
 		// off).
 		int32_t mring[RMAX], oring[RMAX], lring[RMAX];  // the rounds' ring-sourced matches
+		// settle the HBM match loads in every lane: their first uses below
+		// are lane-divergent, and a load left pending on the path that skips
+		// them makes each later reuse of its registers wait vmcnt(0) (one
+		// showed up inside the near-match loop)
+		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #ifndef LZ4ADA_IDX_EXP_NOHBMST
 		// pieces of HBM-sourced matches beyond the first GC, dealt and
 		// loaded in P (the first 64 of the batch)
@@ -1567,6 +1590,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 							ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
 						}
 					}
+					// settle this rare path's loads (see fetch4)
+					__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 				}
 				mring[r] = mdst;
 				oring[r] = off;
