@@ -1495,17 +1495,22 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		}
 		ISTAMP(D_TLDS);
 
-		// L: literals (input ring -> output ring).  Short runs lane by lane;
-		// when a run is over 32 bytes, the 16-byte pieces of both rounds
-		// are dealt over the wave together (one chunk of 64 pieces fewer
-		// per batch than round by round), each piece reading its run from
-		// an LDS descriptor.  (Storing a short last piece as 16 bytes that
-		// spill into its own match, rewritten in M, measured no faster.)
+		// L: literals (input ring -> output ring).  Every run's first 16
+		// bytes in its own lane; the pieces beyond (runs over 16 bytes) of
+		// both rounds are dealt over the wave together, each piece reading
+		// its run from an LDS descriptor.  (Storing a short last piece as 16
+		// bytes that spill into its own match, rewritten in M, measured no
+		// faster.)
 #ifndef LZ4ADA_IDX_EXP_NOLIT
 		static_assert(RMAX == 2, "literal dealing pairs two rounds");
 		{
-			const int32_t nc0 = (rL[0] + 15) >> 4, nc1 = (rL[1] + 15) >> 4;  // rL = 0: no sequence
-			if (__any(nc0 > 2 || nc1 > 2)) {
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r)
+				if (rL[r] > 0)  // rL = 0 also where a round has no sequence
+					ostore(D, rdst[r], fetch16(S, rlit[r]), min(16, rL[r]));
+			const int32_t nc0 = rL[0] > 16 ? (rL[0] - 1) >> 4 : 0;
+			const int32_t nc1 = rL[1] > 16 ? (rL[1] - 1) >> 4 : 0;
+			if (__any(nc0 > 0 || nc1 > 0)) {
 				const int32_t inc0 = wave_incl_scan(nc0);
 				const int32_t tot0 = __shfl(inc0, 63);
 				const int32_t inc1 = tot0 + wave_incl_scan(nc1);
@@ -1523,15 +1528,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					const int32_t lit = base + int32_t(dd & 0xffffu);
 					const int32_t dst = o_batch + int32_t((dd >> 16) & 0xffffu);
 					const int32_t L = int32_t((dd >> 32) & 0xffffu);
-					const int32_t k = t - int32_t(dd >> 48);
+					const int32_t k = 1 + t - int32_t(dd >> 48);  // piece 0 went in-lane
 					if (t < tot)
 						ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, L - 16 * k));
 				}
-			} else {
-#pragma unroll
-				for (int r = 0; r < RMAX; ++r)
-					for (int32_t c = 0; c < rL[r]; c += 16)
-						ostore(D, rdst[r] + c, fetch16(S, rlit[r] + c), min(16, rL[r] - c));
 			}
 		}
 #endif
