@@ -1068,10 +1068,12 @@ __device__ __forceinline__ int32_t ring_pieces(DecLds& D, const int32_t (&mdst)[
 		// source bytes read: the whole period for patterns and overlaps
 		const int32_t s_lo = (opat || wide) ? od - ooff : od - ooff + 16 * k;
 		const int32_t s_hi = (opat || wide) ? od : s_lo + pn;
-		// lanes of this chunk whose piece [pd, pd + 16) meets [s_lo, s_hi):
+		// lanes of this chunk whose piece [pd, pd + pn) meets [s_lo, s_hi):
 		// pd is monotone over the lanes, so two binary searches -- skipped
 		// when every source ends before the chunk's first piece
-		const int32_t pe = act ? pd + 16 : INT32_MAX, ps = act ? pd : INT32_MAX;
+		// a piece writes [pd, pd + pn): its end, not pd + 16 (a short last piece
+		// must not hold back a source that only starts after it)
+		const int32_t pe = act ? pd + pn : INT32_MAX, ps = act ? pd : INT32_MAX;
 		uint64_t dep = 0;
 #ifdef LZ4ADA_IDX_EXP_NODEP  // timing experiment (wrong output): no dependency order
 		if (false) {
