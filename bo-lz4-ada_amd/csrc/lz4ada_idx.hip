@@ -432,15 +432,14 @@ __device__ __forceinline__ int32_t wave_incl_max(int32_t v)
 	return v;
 }
 
-__global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame, uint64_t frame_len,
-                                               const lz4ada_block_desc* __restrict__ desc,
-                                               uint32_t nblocks, uint8_t* __restrict__ tab_all,
-                                               lz4ada_block_status* __restrict__ status)
+// Pass 1 of block b (the body of k_index; k_decode_idx mode 3 runs it
+// before pass 2 of the same block).
+__device__ __forceinline__ void index_block(IdxLds& X, const uint8_t* __restrict__ frame,
+                                            uint64_t frame_len,
+                                            const lz4ada_block_desc* __restrict__ desc, uint32_t b,
+                                            uint8_t* __restrict__ tab_all,
+                                            lz4ada_block_status* __restrict__ status)
 {
-	__shared__ IdxLds X;
-	const uint32_t b = blockIdx.x;
-	if (b >= nblocks)
-		return;
 	const int32_t lane = int32_t(lane_id());
 	const lz4ada_block_desc d = desc[b];
 	if (d.flags & LZ4ADA_BLOCK_STORED) {
@@ -595,6 +594,16 @@ __global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame,
 	if (lane == 0)
 		status[b].code = bad ? DS_RETRY : DS_OK;
 	ISTAMP_FLUSH();
+}
+
+__global__ __launch_bounds__(64) void k_index(const uint8_t* __restrict__ frame, uint64_t frame_len,
+                                               const lz4ada_block_desc* __restrict__ desc,
+                                               uint32_t nblocks, uint8_t* __restrict__ tab_all,
+                                               lz4ada_block_status* __restrict__ status)
+{
+	__shared__ IdxLds X;
+	if (blockIdx.x < nblocks)
+		index_block(X, frame, frame_len, desc, blockIdx.x, tab_all, status);
 }
 
 // ------------------------------------------------------------------ pass 2
@@ -1679,13 +1688,28 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_idx(const uint8_t* __restrict__ frame,
                                                     uint64_t frame_len,
                                                     const lz4ada_block_desc* __restrict__ desc,
-                                                    uint32_t nblocks, const uint8_t* __restrict__ tab_all,
+                                                    uint32_t nblocks, uint8_t* __restrict__ tab_all,
                                                     uint8_t* __restrict__ out,
                                                     lz4ada_block_status* __restrict__ status,
                                                     int linked)
 {
-	__shared__ DecLds D;
-	// one call site of decode_block for both modes (code size)
+	__shared__ union {
+		DecLds d;
+		IdxLds x;
+	} U;
+	DecLds& D = U.d;
+	if (linked == 3) {
+		// fused: pass 1 of this block first (its table and status, read
+		// below by this same wave, made visible first), so a block's pass 2
+		// starts when its own pass 1 is done, not when every block's is
+		if (blockIdx.x < nblocks)
+			index_block(U.x, frame, frame_len, desc, blockIdx.x, tab_all, status);
+		vm_wait();
+		__threadfence();
+		__syncthreads();
+		linked = 0;
+	}
+	// one call site of decode_block for every mode (code size)
 	int64_t hist = linked == 2 ? LINK_HIST : 0;
 	uint32_t b = linked == 1 ? 0u : blockIdx.x;
 	const uint32_t bend = linked == 1 ? nblocks : min(blockIdx.x + 1u, nblocks);
@@ -1756,7 +1780,7 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 	if (nblocks == 0)
 		return hipSuccess;
 	hipLaunchKernelGGL(idx::k_decode_idx, dim3(mode == 1 ? 1 : nblocks), dim3(64), 0, stream, d_frame,
-	                   frame_len, d_desc, nblocks, d_tab, d_out, d_status, mode);
+	                   frame_len, d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status, mode);
 	return hipGetLastError();
 }
 
@@ -1770,11 +1794,16 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 	hipError_t err = hipMallocAsync(&tab, index_table_bytes(frame_len, nblocks), stream);
 	if (err != hipSuccess)
 		return err;
-	err = launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab), d_status,
-	                   stream);
-	if (err == hipSuccess)
+	if (linked == 0) {  // both passes in one launch (mode 3)
 		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
-		                            static_cast<const uint8_t*>(tab), d_out, d_status, linked, stream);
+		                            static_cast<const uint8_t*>(tab), d_out, d_status, 3, stream);
+	} else {
+		err = launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab), d_status,
+		                   stream);
+		if (err == hipSuccess)
+			err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
+			                            static_cast<const uint8_t*>(tab), d_out, d_status, linked, stream);
+	}
 	const hipError_t e2 = hipFreeAsync(tab, stream);
 	return err != hipSuccess ? err : e2;
 }

@@ -111,7 +111,9 @@ hipError_t launch_index(const uint8_t* d_frame, uint64_t frame_len, const lz4ada
                         hipStream_t stream);
 // Pass 2 over a table from launch_index.  mode 0: independent blocks; 1:
 // the serial linked decoder (one workgroup, blocks in order); 2: every
-// block at once with LINK_HIST readable history bytes before its slot.
+// block at once with LINK_HIST readable history bytes before its slot; 3:
+// independent blocks, each wave running pass 1 of its block first (d_tab
+// is written: no launch_index needed).
 hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                  const uint8_t* d_tab, uint8_t* d_out,

@@ -2300,14 +2300,19 @@ hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
 	err = hipEventRecord(side->fork, stream);
 	if (err == hipSuccess)
 		err = hipStreamWaitEvent(side->s, side->fork, 0);
+	// pass 1 and pass 2 in one launch (k_decode_idx mode 3), or as two
+	// (LZ4ADA_NO_FUSE, for A/B)
+	static const bool fuse = getenv("LZ4ADA_NO_FUSE") == nullptr;
 	if (err == hipSuccess)
-		err = launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab), d_status,
-		                   stream);
+		err = fuse ? launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
+		                                   static_cast<const uint8_t*>(tab), d_out, d_status, 3, stream)
+		           : launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab),
+		                          d_status, stream);
 	if (err == hipSuccess)
 		err = launch_block_checksums(d_frame, d_desc, nblocks, d_status, side->s);
 	if (err == hipSuccess)
 		err = hipEventRecord(side->join, side->s);
-	if (err == hipSuccess)
+	if (err == hipSuccess && !fuse)
 		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
 		                            static_cast<const uint8_t*>(tab), d_out, d_status, 0, stream);
 	if (err == hipSuccess)

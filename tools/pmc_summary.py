@@ -96,6 +96,10 @@ def main():
         for f in ("hbm_bytes_per_launch", "fetch_bytes_x2", "write_bytes", "avg_ns"):
             if f in a and f in b:
                 dec[f] = a[f] + b[f]
+    elif "k_decode_idx" in ks:
+        # fused (k_decode_idx mode 3 runs pass 1 too): one kernel
+        dname = "k_decode_idx"
+        dec = ks[dname]
     else:
         dname = next((k for k in ("k_decode_pc", "k_decode_blocks") if k in ks), None)
         dec = ks.get(dname, {})
