@@ -359,10 +359,18 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 		if (c >= 0xFFFFu)
 			ghi[2 * k] = c;
 	};
+	// the dword pair at pos, shifted to pos (LDS; a position outside the
+	// staged window reads garbage, which parse_fast's window test rejects)
+	auto pair_at = [&](int32_t pos) -> uint32_t {
+		const uint32_t a = uint32_t(pos + S.mis) & S.mask;
+		const uint32_t* wa = reinterpret_cast<const uint32_t*>(S.lds + (a & ~3u));
+		return __builtin_amdgcn_alignbyte(wa[1], wa[0], a & 3u);
+	};
 	int32_t p = e;
 	int32_t kc = -1, nxt = 0;  // sub-segment being counted; next record to write
 	uint32_t bm = 0, cnt = 0;
 	bool merged = false;
+	uint32_t w = p < seg_end ? pair_at(p) : 0u;  // token pair of the sequence at p
 	while (p < seg_end) {
 		const int32_t k = (p - s) >> 5;
 		if (k != kc) {
@@ -382,14 +390,32 @@ __device__ __forceinline__ int32_t walk_segment(const Src& S, int32_t e, int32_t
 			merged = true;  // rb[k] is still the previous walk's record
 		bm |= bit;
 		++nst;
+		// parse_fast from the token pair in hand; the offset pair at x and
+		// the next sequence's token pair load together (the next position
+		// needs only this token), so a step waits for one LDS round trip
+		const uint32_t tk = w & 0xffu, e1 = (w >> 8) & 0xffu;
+		const bool x1 = tk >= 0xf0u, x2 = (tk & 15u) == 15u;
+		const int32_t L = int32_t(tk >> 4) + (x1 ? int32_t(e1) : 0);
+		const int32_t x = p + 1 + (x1 ? 1 : 0) + L;
+		const int32_t np = x + 2 + (x2 ? 1 : 0);
+		const uint32_t w2 = pair_at(x), wn = pair_at(np);
+		const uint32_t e2 = (w2 >> 16) & 0xffu;
 		Seq q;
-		if (!parse_fast(S, p, n, q)) {
-			err = true;
-			epos = p;
-			return seg_end;
+		q.L = L;
+		q.ml = int32_t(tk & 15u) + 4 + (x2 ? int32_t(e2) : 0);
+		q.next = np;
+		const bool ok = p >= S.lo && x + 8 <= S.hi && x + 8 <= n && !(x1 && e1 == 255u) &&
+		                !(x2 && e2 == 255u) && (w2 & 0xffffu) != 0;
+		if (!ok) {  // rare shapes (and malformed data): the exact parse
+			if (!parse_seq(S, p, n, q)) {
+				err = true;
+				epos = p;
+				return seg_end;
+			}
 		}
 		cnt += uint32_t(q.L + q.ml);
 		p = q.next;
+		w = ok ? wn : pair_at(p);
 	}
 	if (kc >= 0)
 		put(kc, bm, cnt);
