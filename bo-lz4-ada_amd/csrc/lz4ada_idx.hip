@@ -1726,12 +1726,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	DecLds& D = U.d;
 	if (linked == 3) {
 		// fused: pass 1 of this block first (its table and status, read
-		// below by this same wave, made visible first), so a block's pass 2
+		// below by this same wave, made visible to it first), so a block's pass 2
 		// starts when its own pass 1 is done, not when every block's is
 		if (blockIdx.x < nblocks)
 			index_block(U.x, frame, frame_len, desc, blockIdx.x, tab_all, status);
+		// workgroup scope is enough (the same wave reads it back); an agent
+		// fence here wrote the whole L2 back once per block
 		vm_wait();
-		__threadfence();
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 		__syncthreads();
 		linked = 0;
 	}
