@@ -1133,7 +1133,13 @@ __device__ __forceinline__ int32_t ring_pieces(DecLds& D, const int32_t (&mdst)[
 			if (pm == 0)
 				break;
 			const bool ready = pend && (dep & pm) == 0;
+#ifdef LZ4ADA_IDX_EXP_RINGNOBODY  // timing experiment (wrong output): steps without loads/stores
+			if (ready)
+				asm volatile("" ::"v"(pd), "v"(s_lo));
+			if (false) {
+#else
 			if (ready) {
+#endif
 				// one load for every form (divergent per-form loads made a
 				// step run up to three of them one after the other)
 				int32_t rem = 0;
