@@ -405,6 +405,9 @@ struct lz4ada_decompressor {
 	DevBuf<SerialState> d_serial;
 	DevBuf<lz4ada_block_desc> d_desc;  // one-block fast path
 	DevBuf<lz4ada_block_status> d_bst;
+	DevBuf<uint8_t> d_scr;  // its output, until the block checksum has passed
+	hipStream_t side = nullptr;  // the block checksum, beside the fast decode
+	hipEvent_t ev_in = nullptr;
 
 	// Read-ahead: when one Update call hands over several
 	// complete blocks, they are decoded together by the bulk decoder and
@@ -429,6 +432,12 @@ struct lz4ada_decompressor {
 	lz4ada_decompressor() { lz4ada_xxh32_reset(&hash_all, 0); }
 	~lz4ada_decompressor()
 	{
+		if (side) {
+			(void)hipStreamSynchronize(side);
+			(void)hipStreamDestroy(side);
+		}
+		if (ev_in)
+			(void)hipEventDestroy(ev_in);
 		if (stream) {
 			(void)hipStreamSynchronize(stream);
 			(void)hipStreamDestroy(stream);
@@ -442,6 +451,8 @@ struct lz4ada_decompressor {
 		device_check_or_raise();
 		HIP_OK(hipGetDevice(&device));
 		HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+		HIP_OK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+		HIP_OK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
 		d_tmp_hash.reserve(1);
 		d_serial.reserve(1);
 		d_desc.reserve(1);
@@ -592,20 +603,33 @@ struct lz4ada_decompressor {
 		d_blk.reserve(size_t(std::max<int64_t>(blen, 1)));
 		if (blen > 0)
 			HIP_OK(hipMemcpyAsync(d_blk.p, blk, size_t(blen), hipMemcpyHostToDevice, stream));
-		if (bcl > 0) {  // Check_Checksum before decoding (:672-676, quirk Q8)
-			lz4ada_xxh32_state h;
+		// Check_Checksum comes before decoding (:672-676, quirk Q8): the
+		// checksum (one serial chain) runs on the side stream while the fast
+		// decode writes a scratch slot, and the mirror only takes the output
+		// once the checksum has passed
+		lz4ada_xxh32_state h;
+		if (bcl > 0) {
 			lz4ada_xxh32_reset(&h, 0);
 			HIP_OK(hipMemcpyAsync(d_tmp_hash.p, &h, sizeof h, hipMemcpyHostToDevice, stream));
-			HIP_OK(launch_xxh32_update(d_tmp_hash.p, d_blk.p, uint64_t(raw_len), stream));
-			HIP_OK(hipMemcpyAsync(&h, d_tmp_hash.p, sizeof h, hipMemcpyDeviceToHost, stream));
-			HIP_OK(hipStreamSynchronize(stream));
+			HIP_OK(hipEventRecord(ev_in, stream));
+			HIP_OK(hipStreamWaitEvent(side, ev_in, 0));
+			HIP_OK(launch_xxh32_update(d_tmp_hash.p, d_blk.p, uint64_t(raw_len), side));
+		}
+		const int64_t fast_start = launch_fast_block(raw_len, blen, buflen);
+		if (bcl > 0) {
+			// after the decode launch: a copy into pageable memory returns
+			// only once it is done
+			HIP_OK(hipMemcpyAsync(&h, d_tmp_hash.p, sizeof h, hipMemcpyDeviceToHost, side));
+			HIP_OK(hipStreamSynchronize(side));
 			const uint32_t expect = load32(blk + blen - bcl);
-			if (h.hash != expect)
+			if (h.hash != expect) {
+				HIP_OK(hipStreamSynchronize(stream));  // the scratch decode, discarded
 				raise(LZ4ADA_CHECKSUM_ERROR, "Declared checksum is 0x" + hex32(expect) +
 				                                     ", but computed one is 0x" + hex32(h.hash) +
 				                                     ".");
+			}
 		}
-		if (try_fast_block(raw_len, blen, buflen, first, last)) {
+		if (fast_start >= 0 && finish_fast_block(fast_start, first, last)) {
 			deliver(buf, first, last);
 			return;
 		}
@@ -660,32 +684,38 @@ struct lz4ada_decompressor {
 		return DEC_WG;
 	}
 
-	// Decompress_Full_Block through the bulk decoder for one block: the
-	// block's output goes to the Buffer mirror at the position the reference
-	// would use.  Any status but OK -- including a reference before the
-	// block start, which only the exact path resolves (history scheme,
-	// D1) -- or a content-size overrun leaves the block to k_serial_block,
-	// which redoes it from the same state; the bulk decoder stops at the
-	// first such sequence, so the history that re-run reads is untouched.
-	bool try_fast_block(int64_t raw_len, int64_t blen, int64_t buflen, int64_t& first,
-	                    int64_t& last)
+	// Decompress_Full_Block through the bulk decoder for one block, into a
+	// scratch slot; a clean result moves to the Buffer mirror at the
+	// position the reference would use.  Any status but OK -- including a
+	// reference before the block start, which only the exact path resolves
+	// (history scheme, D1) -- or a content-size overrun leaves the block to
+	// k_serial_block, which redoes it from the same state on an untouched
+	// mirror.  launch_fast_block enqueues the decode and returns the block's
+	// Output_Pos (-1: not tried); finish_fast_block waits for it.
+	int64_t launch_fast_block(int64_t raw_len, int64_t blen, int64_t buflen)
 	{
 		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
 		if (linked || getenv("LZ4ADA_FACADE_EXACT"))
-			return false;
+			return -1;
 		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;  // :678-680
 		const int64_t cap = std::min<int64_t>(buflen - start, INT32_MAX);
 		if (cap <= 0 || raw_len > INT32_MAX)
-			return false;
+			return -1;
+		d_scr.reserve(size_t(cap));
 		lz4ada_block_desc d{};
 		d.in_off = 0;
 		d.in_len = uint32_t(raw_len);
 		d.flags = m.is_compressed ? 0u : LZ4ADA_BLOCK_STORED;
-		d.out_off = uint64_t(start);
+		d.out_off = 0;
 		d.out_cap = uint32_t(cap);
 		HIP_OK(hipMemcpyAsync(d_desc.p, &d, sizeof d, hipMemcpyHostToDevice, stream));
 		HIP_OK(launch_decode_variant(d_blk.p, uint64_t(std::max<int64_t>(blen, 1)), d_desc.p, 1,
-		                             d_buf.p, d_bst.p, facade_variant(), stream));
+		                             d_scr.p, d_bst.p, facade_variant(), stream));
+		return start;
+	}
+
+	bool finish_fast_block(int64_t start, int64_t& first, int64_t& last)
+	{
 		lz4ada_block_status st;
 		HIP_OK(hipMemcpyAsync(&st, d_bst.p, sizeof st, hipMemcpyDeviceToHost, stream));
 		HIP_OK(hipStreamSynchronize(stream));
@@ -696,6 +726,9 @@ struct lz4ada_decompressor {
 			return false;  // the exact path raises mid-block, as the reference does
 		if (m.has_content_size)
 			m.size_remaining -= uint64_t(nout);
+		if (nout > 0)  // deliver() reads it from the mirror, after this copy
+			HIP_OK(hipMemcpyAsync(d_buf.p + start, d_scr.p, size_t(nout), hipMemcpyDeviceToDevice,
+			                      stream));
 		output_pos = start + nout;
 		if (output_pos >= HISTORY_SIZE)  // :785-787 (:688-690 for stored blocks)
 			output_pos_history = output_pos;

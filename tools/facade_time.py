@@ -41,16 +41,20 @@ def main():
     ap.add_argument("--block-max", type=int, default=4 << 20)
     ap.add_argument("--feed", type=int, default=0)
     ap.add_argument("--indep", type=int, default=1)
+    ap.add_argument("--bcksum", type=int, default=1, help="block checksums in the frame")
+    ap.add_argument("--ccksum", type=int, default=1, help="content checksum in the frame")
     args = ap.parse_args()
     blocks = []
     for i in range(args.blocks):
         comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[args.kind], 0x4C5A3441 + i, args.block_max)
         blocks.append((comp, raw, False))
     frame, expect = lz4frame.build_frame(blocks, args.block_max, indep=bool(args.indep),
-                                         block_cksum=True, content_cksum=True)
+                                         block_cksum=bool(args.bcksum),
+                                          content_cksum=bool(args.ccksum))
     run(frame, expect, args.feed)  # warm
     dt = run(frame, expect, args.feed)
-    print(f"facade {args.kind} feed={args.feed} {args.blocks}x{args.block_max >> 10} KiB: "
+    print(f"facade {args.kind} feed={args.feed} bcksum={args.bcksum} ccksum={args.ccksum} "
+          f"{args.blocks}x{args.block_max >> 10} KiB: "
           f"{dt * 1e3:.1f} ms  {len(expect) / dt / 2**20:.1f} MiB/s")
 
 
