@@ -7,48 +7,46 @@ checksum (XXH32 of each compressed payload, lz4ada.adb:698-707) and the
 GPU block decoder (lz4ada.adb:716-904), input already resident in HBM,
 output left in HBM.
 
-Workload (config.workload): BASELINE.json configs[3] shape -- 4 MiB blocks,
-FLG 0x70 (version 01 | B.Indep | B.Checksum), BD 0x70 (4 MiB) -- with a
-fixed shard of 2048 blocks (8 GiB decoded, the size of configs[2]) per GPU,
-so N GPUs decode an N x 8 GiB frame (weak scaling; N = 4 is configs[3]'s
-32 GiB).  The frame has no content checksum, so nothing is skipped; the
-content-checksum variant (configs[2], FLG 0x74) is reported separately as
-`e2e_content_checksum` because a frame-wide XXH32 is one serial chain
-(SURVEY §7 H2).
+Workloads (config.workload):
+* N = 1 (the default): 2048 x 4 MiB blocks = 8 GiB decoded, FLG 0x70
+  (version 01 | B.Indep | B.Checksum), BD 0x70 -- configs[2]'s size, the
+  HBM roofline run.  The content-checksum variant (configs[2], FLG 0x74) is
+  reported separately as `e2e_content_checksum`: a frame-wide XXH32 is one
+  serial chain.
+* N > 1: configs[3] itself -- a 32 GiB frame (8192 x 4 MiB blocks, FLG
+  0x70) split into N contiguous block ranges, one per rank (strong
+  scaling); `value` is the whole frame's decoded bytes / max-over-ranks
+  time.  `--gpus N` starts the N ranks itself (torch.distributed.run, one
+  process per GPU, RCCL) unless it already runs under a launcher.
 
 Synthetic data: 64 unique blocks from the repo's deterministic LZ4
-sequence generator (seed 0x4C5A3441 + i), tiled to size on the device.
-Golden check: per-block XXH32 of every decoded slot (on the GPU) against
-the generator's plaintext hash, after the warmup.
+sequence generator (seed 0x4C5A3441 + i), tiled to size; each rank's shard
+is assembled in host memory and copied to the GPU once.  Golden check:
+per-block XXH32 of every decoded slot (on the GPU) against the generator's
+plaintext hash, after the warmup.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL); blocks shard
-across ranks with no data-path collective.  Timing: barrier +
-synchronize on both sides of exactly K steps, max over ranks.
+across ranks with no data-path collective (SURVEY §8e).  Timing: barrier +
+synchronize on both sides of exactly K steps, max over ranks.  The one
+status all-reduce (MAX) runs after the timed region.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "bo-lz4-ada_amd"))
 
-import torch  # noqa: E402  (load torch's HIP runtime before liblz4ada_hip.so)
-import torch.distributed as dist  # noqa: E402
-import xxhash  # noqa: E402
-
-import lz4ada  # noqa: E402
-import lz4frame  # noqa: E402
-
 METRIC = "decompressed MiB/s + achieved HBM GB/s vs roofline, 4MiB-block frame @1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# decode kernel each LZ4ADA_DECODER setting launches (lz4ada_kernels.hip launch_decode_blocks)
-DECODE_KERNEL = {"idx": "k_decode_idx", "pc": "k_decode_pc", "wave": "k_decode_blocks",
-                 "wg": "k_decode_wg"}
 SEED0 = 0x4C5A3441
 MiB = 1 << 20
+C3_BLOCKS = 8192  # configs[3]: 32 GiB of 4 MiB blocks
 
 
 def log(*a):
@@ -56,30 +54,91 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def make_unique_blocks(kind, n_unique, block_max):
-    """-> list of (record bytes incl. size word + checksum, payload len, raw len, raw xxh32)."""
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kind", default="mixed")
+    ap.add_argument("--blocks", type=int, default=0,
+                    help="blocks of the whole frame (default: 2048 at N=1, configs[3]'s 8192 "
+                         "split over the ranks at N>1)")
+    ap.add_argument("--block-max", type=int, default=4 * MiB)
+    ap.add_argument("--unique", type=int, default=64)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--classes", default="stored,literal,dense,rle",
+                    help="extra content classes timed through the product call (N=1 only)")
+    ap.add_argument("--no-linked", action="store_true",
+                    help="skip the configs[4] row (1 GiB linked frame, 256 KiB blocks)")
+    ap.add_argument("--no-64k", action="store_true",
+                    help="skip the configs[1] row (1 GiB frame, 64 KiB blocks)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test hook: start the ranks, check the process group (gloo, no GPU), "
+                         "print one JSON line")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_decode.json"))
+    return ap.parse_args(argv)
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """--gpus N outside a launcher: start N ranks with torch.distributed.run
+    (one process per GPU) as a child and return its exit code.  Runs before
+    anything touches the GPU in this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------- synthetic data
+
+def make_unique_blocks(lz4ada, lz4frame, xxhash, kind, n_unique, block_max, block_cksum=True):
+    """-> list of (record bytes incl. size word [+ checksum], payload len,
+    raw len, raw xxh32, payload, raw).  kind "stored": random bytes in
+    uncompressed blocks (size word bit 31, lz4ada.adb:536-538, 686-694)."""
+    import numpy as np
     recs = []
     for i in range(n_unique):
-        comp, raw = lz4ada.gen_block(kind, SEED0 + i, block_max)
-        rec = lz4frame.block_record(comp, stored=False, block_cksum=True)
+        if kind == "stored":
+            raw = np.random.default_rng(SEED0 + i).integers(0, 256, block_max, dtype=np.uint8)
+            comp = raw = raw.tobytes()
+            rec = lz4frame.block_record(comp, stored=True, block_cksum=block_cksum)
+        else:
+            comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[kind], SEED0 + i, block_max)
+            rec = lz4frame.block_record(comp, stored=False, block_cksum=block_cksum)
         recs.append((rec, len(comp), len(raw), xxhash.xxh32(raw).intdigest(), comp, raw))
     return recs
 
 
-def build_shard(recs, first_block, nblocks, block_max, dev):
-    """Tile the unique block records into this rank's shard of the frame."""
+def assemble_shard(lz4ada, torch, recs, first_block, nblocks, block_max, dev):
+    """This rank's shard of the tiled frame, assembled in host memory and
+    copied to the GPU in one transfer (no per-block device copies)."""
+    import numpy as np
     n_unique = len(recs)
     order = [(first_block + i) % n_unique for i in range(nblocks)]
-    offs, pos = [], 0
-    for u in order:
-        offs.append(pos)
-        pos += len(recs[u][0])
+    lens = [len(recs[u][0]) for u in order]
+    offs = [0] * nblocks
+    pos = 0
+    for i, ln in enumerate(lens):
+        offs[i] = pos
+        pos += ln
     frame_len = pos + 64
-    d_frame = torch.empty(frame_len, dtype=torch.uint8, device=dev)
-    d_frame[pos:].zero_()
-    d_unique = [torch.frombuffer(bytearray(r[0]), dtype=torch.uint8).to(dev) for r in recs]
+    host = np.empty(frame_len, dtype=np.uint8)
+    host[pos:] = 0
+    arrs = [np.frombuffer(r[0], dtype=np.uint8) for r in recs]
     for i, u in enumerate(order):
-        d_frame[offs[i]:offs[i] + len(recs[u][0])].copy_(d_unique[u])
+        host[offs[i]:offs[i] + lens[i]] = arrs[u]
+    d_frame = torch.from_numpy(host).to(dev)
+    del host
     descs = (lz4ada.BlockDesc * nblocks)()
     exp_hash = []
     comp_bytes = raw_bytes = 0
@@ -88,20 +147,39 @@ def build_shard(recs, first_block, nblocks, block_max, dev):
         d = descs[i]
         d.in_off = offs[i] + 4
         d.in_len = clen
-        d.flags = lz4ada.BLOCK_HAS_CKSUM
+        stored = (int.from_bytes(rec[:4], "little") >> 31) & 1
+        has_ck = len(rec) == clen + 8
+        d.flags = (lz4ada.BLOCK_STORED if stored else 0) | (lz4ada.BLOCK_HAS_CKSUM if has_ck else 0)
         d.out_off = i * block_max
         d.out_cap = block_max
-        d.cksum = int.from_bytes(rec[4 + clen:8 + clen], "little")
+        d.cksum = int.from_bytes(rec[4 + clen:8 + clen], "little") if has_ck else 0
         exp_hash.append(h)
         comp_bytes += clen
         raw_bytes += rlen
     d_desc = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
     torch.cuda.synchronize()
-    del d_unique
     return d_frame, frame_len, d_desc, exp_hash, comp_bytes, raw_bytes, descs
 
 
-def cpu_baseline_parallel(recs, block_max, threads, blocks_per_thread):
+def check_statuses(lz4ada, d_status, nblocks):
+    return (lz4ada.BlockStatus * nblocks).from_buffer_copy(d_status.cpu().numpy().tobytes())
+
+
+def golden_check(lz4ada, torch, d_status, descs, nb, op, dp, sp, d_hash, exp_hash, sh, what):
+    st = check_statuses(lz4ada, d_status, nb)
+    bad = [i for i in range(nb) if st[i].code != 0 or
+           ((descs[i].flags & lz4ada.BLOCK_HAS_CKSUM) and st[i].cksum != descs[i].cksum)]
+    assert not bad, f"{what}: block status / checksum errors: {bad[:5]}"
+    lz4ada.output_checksums_device(op, dp, sp, nb, d_hash.data_ptr(), sh)
+    torch.cuda.synchronize()
+    got = [h & 0xffffffff for h in d_hash[:nb].cpu().tolist()]
+    assert got == exp_hash, f"{what}: decoded output differs from the generator's plaintext"
+    return st
+
+
+# --------------------------------------------------------------- CPU baseline
+
+def cpu_baseline_parallel(lz4frame, xxhash, recs, block_max, threads, blocks_per_thread):
     """SURVEY §8d's N-core extrapolation for independent frames: `threads`
     threads, each running the oracle's unlz4ada loop (ctypes releases the
     GIL) over its own frame of `blocks_per_thread` independent blocks of the
@@ -142,26 +220,22 @@ def cpu_baseline_parallel(recs, block_max, threads, blocks_per_thread):
                       "loop; block-parallel extrapolation for independent frames (SURVEY §8d)"}
 
 
-def content_hash(recs, nblocks):
-    """Expected frame-wide XXH32 of rank 0's decoded shard (python-xxhash over
-    the generator's plaintext, tiled like build_shard)."""
+def content_hash(xxhash, recs, nblocks, first=0):
+    """Expected frame-wide XXH32 of a decoded shard (python-xxhash over the
+    generator's plaintext, tiled like assemble_shard)."""
     h = xxhash.xxh32()
     for i in range(nblocks):
-        h.update(recs[i % len(recs)][5])
+        h.update(recs[(first + i) % len(recs)][5])
     return h.intdigest()
 
 
-def check_statuses(d_status, nblocks):
-    st = (lz4ada.BlockStatus * nblocks).from_buffer_copy(d_status.cpu().numpy().tobytes())
-    return st
-
-
-def cpu_baseline(recs, block_max, budget_s):
+def cpu_baseline(lz4frame, xxhash, recs, block_max, budget_s):
     """The oracle (lz4ada.adb restated in C, 'port') through the reference's
     CLI loop (tool_unlz4ada: 4 KiB reads, one Update per call), one core,
     on a bounded prefix of the same frame."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
+
     def frame_of(k):
         blocks = [(recs[i % len(recs)][4], recs[i % len(recs)][5], False) for i in range(k)]
         return lz4frame.build_frame(blocks, block_max, indep=True, block_cksum=True)
@@ -192,11 +266,47 @@ def cpu_baseline(recs, block_max, budget_s):
                       "call, block checksums verified)"}
 
 
-def bench_linked(dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, chain=64):
+# ------------------------------------------------------------------ extra rows
+
+def bench_class(M, dev, sh, stream, cls, nb, bmax, block_cksum=True, unique=16):
+    """One more content class over the same layout, timed through the
+    product call (block checksums when the frame has them + decode)."""
+    lz4ada, lz4frame, xxhash, torch = M
+    recs = make_unique_blocks(lz4ada, lz4frame, xxhash, cls, unique, bmax, block_cksum)
+    fr, fl, de, eh, cb, rb, descs = assemble_shard(lz4ada, torch, recs, 0, nb, bmax, dev)
+    d_out = torch.empty(nb * bmax, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
+    d_hash = torch.zeros(nb, dtype=torch.int32, device=dev)
+    fp, dp, op, sp = fr.data_ptr(), de.data_ptr(), d_out.data_ptr(), d_st.data_ptr()
+    lz4ada.decode_blocks_device(fp, fl, dp, nb, op, sp, sh)
+    torch.cuda.synchronize()
+    golden_check(lz4ada, torch, d_st, descs, nb, op, dp, sp, d_hash, eh, sh, cls)
+    reps = 3
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        lz4ada.decode_blocks_device(fp, fl, dp, nb, op, sp, sh)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in ev) / reps
+    flg = 0x60 | (0x10 if block_cksum else 0)
+    row = {"decode_ms": round(ms, 3), "MiB_s": round(rb / (ms * 1e-3) / MiB, 1),
+           "frac": round((cb + rb) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "ratio": round(cb / rb, 4), "flg": f"0x{flg:02x}", "blocks": nb,
+           "compressed_bytes": cb, "decoded_bytes": rb,
+           "golden": "per-block XXH32 of the output vs the generator"}
+    del fr, de, d_out
+    return row
+
+
+def bench_linked(M, dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, chain=64):
     """configs[4]: a linked frame (B.Indep = 0) of 4096 x 256 KiB blocks whose
     matches reach into the previous block: a chain of 64 generated blocks
     (each against the previous one's output), tiled -- the first block of
     the chain has no history references, so every tile boundary is valid."""
+    import numpy as np
+    lz4ada, lz4frame, xxhash, torch = M
     blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS[kind], SEED0, bmax, chain)
     recs = [lz4frame.block_record(c, stored=False, block_cksum=True) for c, _ in blocks]
     hashes = [xxhash.xxh32(r).intdigest() for _, r in blocks]
@@ -205,13 +315,12 @@ def bench_linked(dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, c
     for u in order:
         offs.append(pos)
         pos += len(recs[u])
-    d_frame = torch.empty(pos + 64, dtype=torch.uint8, device=dev)
-    d_frame[pos:].zero_()
-    d_rec = [torch.frombuffer(bytearray(r), dtype=torch.uint8).to(dev) for r in recs]
+    host = np.zeros(pos + 64, dtype=np.uint8)
+    arrs = [np.frombuffer(r, dtype=np.uint8) for r in recs]
     descs = (lz4ada.BlockDesc * nblocks)()
     comp = 0
     for i, u in enumerate(order):
-        d_frame[offs[i]:offs[i] + len(recs[u])].copy_(d_rec[u])
+        host[offs[i]:offs[i] + len(recs[u])] = arrs[u]
         clen = len(blocks[u][0])
         descs[i].in_off = offs[i] + 4
         descs[i].in_len = clen
@@ -220,9 +329,9 @@ def bench_linked(dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, c
         descs[i].out_cap = bmax
         descs[i].cksum = int.from_bytes(recs[u][4 + clen:8 + clen], "little")
         comp += clen
+    d_frame = torch.from_numpy(host).to(dev)
     raw = nblocks * bmax
     d_out = torch.empty(raw, dtype=torch.uint8, device=dev)
-    del d_rec
 
     def run():
         return lz4ada.decode_linked_device(d_frame.data_ptr(), pos + 64, descs, nblocks, bmax,
@@ -252,6 +361,7 @@ def bench_linked(dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, c
     return {"workload": f"configs[4]: linked frame (FLG 0x50: B.Checksum, B.Indep=0), {nblocks} x "
                         f"{bmax >> 10} KiB {kind} blocks, matches reach into the previous block",
             "decode_ms": round(ms, 3), "MiB_s": round(raw / (ms * 1e-3) / MiB, 1),
+            "frac": round((comp + raw) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "compressed_bytes": comp, "decoded_bytes": raw,
             "path": "lz4ada_decode_linked_device: block checksums, k_index, 3 x k_decode_idx "
                     "(every block at once, synthetic history X / ~X / hi), k_link_init + "
@@ -260,25 +370,23 @@ def bench_linked(dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, c
             "golden": "per-block XXH32 of the output vs the generator"}
 
 
-def bench_64k(dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, unique=64):
+def bench_64k(M, dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, unique=64):
     """configs[1]: a 1 GiB frame of 64 KiB independent blocks with a content
     checksum.  The decode launch (block checksums + decode, device-resident)
     is timed with HIP events; the frame-wide content XXH32 (one serial chain,
     SURVEY H2) runs through the D2H + host-chain pipeline and is reported
     beside it."""
-    recs = make_unique_blocks(lz4ada.GEN_KINDS[kind], unique, bmax)
-    d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = build_shard(recs, 0, nblocks, bmax, dev)
+    lz4ada, lz4frame, xxhash, torch = M
+    recs = make_unique_blocks(lz4ada, lz4frame, xxhash, kind, unique, bmax)
+    d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = assemble_shard(
+        lz4ada, torch, recs, 0, nblocks, bmax, dev)
     d_out = torch.empty(nblocks * bmax, dtype=torch.uint8, device=dev)
     d_st = torch.zeros(nblocks * 32, dtype=torch.uint8, device=dev)
     d_hash = torch.zeros(nblocks, dtype=torch.int32, device=dev)
     fp, dp, op, sp = d_frame.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), d_st.data_ptr()
     lz4ada.decode_blocks_device(fp, frame_len, dp, nblocks, op, sp, sh)
     torch.cuda.synchronize()
-    st = check_statuses(d_st, nblocks)
-    assert all(s.code == 0 and s.cksum == descs[i].cksum for i, s in enumerate(st)), "64 KiB frame"
-    lz4ada.output_checksums_device(op, dp, sp, nblocks, d_hash.data_ptr(), sh)
-    torch.cuda.synchronize()
-    assert [h & 0xffffffff for h in d_hash.cpu().tolist()] == exp_hash, "64 KiB frame output"
+    golden_check(lz4ada, torch, d_st, descs, nblocks, op, dp, sp, d_hash, exp_hash, sh, "64 KiB")
     reps = 5
     e0, e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
     e0.record(stream)
@@ -298,7 +406,7 @@ def bench_64k(dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, uniq
     t0 = time.perf_counter()
     h.update_device_d2h(op, raw, None, sh)
     t_hash = time.perf_counter() - t0
-    assert h.final() == content_hash(recs, nblocks), "64 KiB frame content checksum"
+    assert h.final() == content_hash(xxhash, recs, nblocks), "64 KiB frame content checksum"
     del d_frame, d_out
     return {"workload": f"configs[1]: {raw >> 30} GiB frame, {nblocks} x 64 KiB independent "
                         f"{kind} blocks, FLG 0x74 (B.Indep|B.Checksum|C.Checksum)",
@@ -311,25 +419,48 @@ def bench_64k(dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, uniq
             "compressed_bytes": comp, "decoded_bytes": raw}
 
 
+# ----------------------------------------------------------------------- main
+
+def launch_check(args):
+    """--launch-check: the rank side of the launcher test (gloo, no GPU)."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        lo, hi = shard_range(rank, world, args.blocks or C3_BLOCKS)
+        import torch
+        t = torch.tensor([hi - lo], dtype=torch.int64)
+        dist.all_reduce(t)
+        total = int(t.item())
+        dist.destroy_process_group()
+    else:
+        total = args.blocks or 2048
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks": world, "blocks_total": total}), flush=True)
+
+
+def shard_range(rank, world, total):
+    """Contiguous block range [lo, hi) of `rank` (configs[3]'s split)."""
+    lo = total * rank // world
+    hi = total * (rank + 1) // world
+    return lo, hi
+
+
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--kind", default="mixed", choices=sorted(lz4ada.GEN_KINDS))
-    ap.add_argument("--blocks-per-gpu", type=int, default=2048)
-    ap.add_argument("--block-max", type=int, default=4 * MiB)
-    ap.add_argument("--unique", type=int, default=64)
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--classes", default="", help="extra classes to time, e.g. dense,rle,literal")
-    ap.add_argument("--no-linked", action="store_true",
-                    help="skip the configs[4] row (1 GiB linked frame, 256 KiB blocks)")
-    ap.add_argument("--no-64k", action="store_true",
-                    help="skip the configs[1] row (1 GiB frame, 64 KiB blocks)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_decode.json"))
-    args = ap.parse_args()
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.launch_check:
+        return launch_check(args)
+
+    import torch  # noqa: E402  (torch's HIP runtime before liblz4ada_hip.so)
+    import torch.distributed as dist  # noqa: E402
+    import xxhash  # noqa: E402
+    import lz4ada  # noqa: E402
+    import lz4frame  # noqa: E402
+    M = (lz4ada, lz4frame, xxhash, torch)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -337,6 +468,9 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world
+        if args.gpus not in (1, world):
+            raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
@@ -351,20 +485,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    nb = args.blocks_per_gpu
     bmax = args.block_max
-    kind = lz4ada.GEN_KINDS[args.kind]
-    log(f"[bench] generating {args.unique} unique {args.kind} blocks ...")
-    recs = make_unique_blocks(kind, args.unique, bmax)
-    d_frame, frame_len, d_desc, exp_hash, comp_bytes, raw_bytes, descs = build_shard(
-        recs, rank * nb, nb, bmax, dev)
+    total_blocks = args.blocks or (2048 if world == 1 else C3_BLOCKS)
+    lo, hi = shard_range(rank, world, total_blocks)
+    nb = hi - lo
+    log(f"[bench] {world} rank(s), frame of {total_blocks} x {bmax >> 20} MiB blocks; "
+        f"generating {args.unique} unique {args.kind} blocks ...")
+    recs = make_unique_blocks(lz4ada, lz4frame, xxhash, args.kind, args.unique, bmax)
+    d_frame, frame_len, d_desc, exp_hash, comp_bytes, raw_bytes, descs = assemble_shard(
+        lz4ada, torch, recs, lo, nb, bmax, dev)
     d_out = torch.empty(nb * bmax, dtype=torch.uint8, device=dev)
     d_status = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
     d_hash = torch.zeros(nb, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     fp, dp, op, sp = d_frame.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), d_status.data_ptr()
-    log(f"[bench] shard: {nb} blocks, {comp_bytes / MiB:.0f} MiB compressed -> "
+    log(f"[bench] rank shard: blocks [{lo}, {hi}), {comp_bytes / MiB:.0f} MiB compressed -> "
         f"{raw_bytes / MiB:.0f} MiB decoded")
 
     def step(events=None):
@@ -380,13 +516,8 @@ def main():
         step()
     torch.cuda.synchronize()
     # ---- golden check (outside the timed region)
-    st = check_statuses(d_status, nb)
-    bad = [i for i in range(nb) if st[i].code != 0 or st[i].cksum != descs[i].cksum]
-    assert not bad, f"block status / checksum errors: {bad[:5]}"
-    lz4ada.output_checksums_device(op, dp, sp, nb, d_hash.data_ptr(), sh)
-    torch.cuda.synchronize()
-    got = [h & 0xffffffff for h in d_hash.cpu().tolist()]
-    assert got == exp_hash, "decoded output differs from the generator's plaintext"
+    st = golden_check(lz4ada, torch, d_status, descs, nb, op, dp, sp, d_hash, exp_hash, sh,
+                      "headline")
     assert sum(s.out_len for s in st) == raw_bytes
     log("[bench] golden check passed (per-block XXH32 of output, block checksums)")
 
@@ -403,8 +534,15 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed)
     dec_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    st = check_statuses(d_status, nb)
-    assert all(s.code == 0 for s in st)
+    # the one status collective (all-reduce MAX of the block
+    # statuses), after the timed region
+    st = check_statuses(lz4ada, d_status, nb)
+    local_bad = int(any(s.code != 0 for s in st))
+    if world > 1:
+        t = torch.tensor([local_bad], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        local_bad = int(t.item())
+    assert local_bad == 0
     # the two halves alone (after the timed region, same stream): what the
     # overlap hides
     alone = {}
@@ -420,9 +558,11 @@ def main():
         alone[name] = round(sum(a.elapsed_time(b) for a, b in a_ev) / len(a_ev), 3)
 
     ms_per_step = elapsed / args.steps * 1e3
-    total_raw = raw_bytes * world * args.steps
-    value = total_raw / elapsed / MiB
-    dec_kernel = DECODE_KERNEL[os.environ.get("LZ4ADA_DECODER", "idx")]
+    # the whole frame's bytes (every rank's shard; the tiling is deterministic)
+    total_raw = sum(recs[i % len(recs)][2] for i in range(total_blocks))
+    frame_alg = total_raw + sum(recs[i % len(recs)][1] for i in range(total_blocks))
+    value = total_raw * args.steps / elapsed / MiB
+    dec_kernel = "k_decode_idx"
     alg_bytes = comp_bytes + raw_bytes  # compressed read once + output written once
     achieved = alg_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None
@@ -435,37 +575,48 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "kernel": dec_kernel, "kernel_ms": round(dec_ms, 3),
-            "kernel_ms_note": "HIP events around lz4ada_decode_blocks_device on its stream: "
-                              "k_decode_idx (pass 1 then pass 2 of each block in one wave) with "
-                              "k_xxh32_rows (block checksums) overlapped on the side stream",
+            "kernel_ms_note": "HIP events (rank 0) around lz4ada_decode_blocks_device on its "
+                              "stream: k_decode_idx (pass 1 then pass 2 of each block in one "
+                              "wave) with k_xxh32_rows (block checksums) overlapped on the side "
+                              "stream",
             "alg_bytes_per_launch": alg_bytes,
             "alone_ms": alone}
 
+    if world > 1:
+        workload = (f"configs[3]: {total_blocks * bmax >> 30} GiB frame, {total_blocks} x 4 MiB "
+                    f"independent blocks, FLG 0x70 (B.Indep|B.Checksum), BD 0x70, split into "
+                    f"{world} contiguous block ranges (one per GPU)")
+    else:
+        workload = (f"configs[2] size, configs[3] shape: {total_blocks} x 4 MiB independent "
+                    f"blocks = {raw_bytes >> 30} GiB decoded, FLG 0x70 (B.Indep|B.Checksum), "
+                    "BD 0x70 (content-checksum variant FLG 0x74: e2e_content_checksum)")
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "MiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic: repo LZ4 sequence generator, 64 unique blocks tiled on device",
-        "config": {"workload": "configs[3] shape per GPU: 4 MiB independent blocks, FLG 0x70 "
-                               "(B.Indep|B.Checksum), BD 0x70; 2048 blocks = 8 GiB decoded "
-                               "per GPU (configs[2] size)",
-                   "class": args.kind, "blocks_per_gpu": nb, "block_max": bmax,
-                   "compressed_bytes_per_gpu": comp_bytes, "decoded_bytes_per_gpu": raw_bytes,
+        "higher_is_better": True, "scaling": "strong" if world > 1 else "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: repo LZ4 sequence generator, 64 unique blocks tiled in host memory",
+        "config": {"workload": workload, "class": args.kind, "blocks_total": total_blocks,
+                   "blocks_per_gpu": nb, "block_max": bmax,
+                   "compressed_bytes_rank0": comp_bytes, "decoded_bytes_rank0": raw_bytes,
                    "parallelism": f"block-shard x{world}"},
-        "hbm_gbps_step": round((comp_bytes + raw_bytes) * world / (elapsed / args.steps) / 1e9, 1),
+        "hbm_gbps_step": round(frame_alg / (elapsed / args.steps) / 1e9, 1),
         "roofline": roof,
     }
+    if world > 1:
+        result["rccl_ranks"] = dist.get_world_size()
 
+    extra = world == 1 and rank == 0
     # ---- configs[2] e2e: + frame-wide content XXH32 (one serial chain), run
     # by the D2H + host-chain pipeline (lz4ada_content_xxh32_d2h) the bulk
     # path uses: chunks are hashed while the next one is in flight
-    if not args.no_e2e and rank == 0:
+    if extra and not args.no_e2e:
         h = lz4ada.XXHash32()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         h.update_device_d2h(op, raw_bytes, None, sh)
         t_hash = time.perf_counter() - t0
-        assert h.final() == content_hash(recs, nb), "content checksum mismatch"
+        assert h.final() == content_hash(xxhash, recs, nb), "content checksum mismatch"
         result["e2e_content_checksum"] = {
             "workload": "configs[2]: same 8 GiB frame with FLG 0x74 (+C.Checksum)",
             "content_xxh32_s": round(t_hash, 3),
@@ -474,46 +625,33 @@ def main():
                     "stream to the host in 32 MiB chunks, each hashed by one host core while "
                     "the next is in flight (one GPU wave runs the chain at ~1.1 GB/s)"}
 
-    # ---- other content classes (fewer steps)
-    extra = {}
-    for cls in [c for c in args.classes.split(",") if c]:
-        recs_c = make_unique_blocks(lz4ada.GEN_KINDS[cls], min(args.unique, 16), bmax)
-        fr, fl, de, eh, cb, rb, _ = build_shard(recs_c, rank * nb, nb, bmax, dev)
-        fpc, dpc = fr.data_ptr(), de.data_ptr()
-        lz4ada.decode_blocks_device(fpc, fl, dpc, nb, op, sp, sh)
-        torch.cuda.synchronize()
-        stc = check_statuses(d_status, nb)
-        assert all(s.code == 0 for s in stc), cls
-        lz4ada.output_checksums_device(op, dpc, sp, nb, d_hash.data_ptr(), sh)
-        torch.cuda.synchronize()
-        assert [h & 0xffffffff for h in d_hash.cpu().tolist()] == eh, cls
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 3
-        e0.record(stream)
-        for _ in range(reps):
-            lz4ada.launch_decode(fpc, fl, dpc, nb, op, sp, sh)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        extra[cls] = {"decode_ms": round(ms, 3), "MiB_s": round(rb / (ms * 1e-3) / MiB, 1),
-                      "frac": round((cb + rb) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                      "ratio": round(cb / rb, 4)}
-        del fr, de
+    # ---- other content classes through the product call, same layout
     if extra:
-        result["classes_decode_kernel"] = extra
+        del d_out
+        rows = {}
+        for cls in [c for c in args.classes.split(",") if c]:
+            if cls == "stored":
+                # README.md:753-766's `random` rows: lz4 CLI defaults, no block checksum
+                rows["stored"] = bench_class(M, dev, sh, stream, "stored", nb, bmax, block_cksum=False)
+                rows["stored_bcksum"] = bench_class(M, dev, sh, stream, "stored", nb, bmax)
+            else:
+                rows[cls] = bench_class(M, dev, sh, stream, cls, nb, bmax)
+        if rows:
+            result["classes"] = rows
 
     # ---- configs[4]: linked (dependent) 256 KiB-block frame, 1 GiB, one GPU:
     # every block at once against synthetic history, resolved on the GPU
-    if rank == 0 and not args.no_linked:
-        result["linked_c5"] = bench_linked(dev, sh, stream)
+    if extra and not args.no_linked:
+        result["linked_c5"] = bench_linked(M, dev, sh, stream)
     # ---- configs[1]: 1 GiB of 64 KiB independent blocks + content checksum
-    if rank == 0 and not args.no_64k:
-        result["c2_64k"] = bench_64k(dev, sh, stream)
+    if extra and not args.no_64k:
+        result["c2_64k"] = bench_64k(M, dev, sh, stream)
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(recs, bmax, args.cpu_budget)
+    if extra and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(lz4frame, xxhash, recs, bmax, args.cpu_budget)
         threads = min(16, os.cpu_count() or 1)
-        result["cpu_baseline_parallel"] = cpu_baseline_parallel(recs, bmax, threads, 64)
+        result["cpu_baseline_parallel"] = cpu_baseline_parallel(lz4frame, xxhash, recs, bmax,
+                                                                threads, 64)
     elif rank == 0:
         result["cpu_baseline"] = None
 

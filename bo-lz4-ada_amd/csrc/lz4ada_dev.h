@@ -63,6 +63,18 @@ __device__ __forceinline__ int32_t wave_incl_scan(int32_t v)
 	return v;
 }
 
+// Inclusive prefix maximum over the wave (values >= 0), DPP as wave_incl_scan.
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v)
+{
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));   // row_shr:1
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));   // row_shr:2
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));   // row_shr:4
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));   // row_shr:8
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+	return v;
+}
+
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
 
 __device__ __forceinline__ void lds_store_n(uint8_t* dst, u32x4 v, int32_t n)

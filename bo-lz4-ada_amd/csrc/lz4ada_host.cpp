@@ -1119,31 +1119,25 @@ int lz4ada_xxh32_update_device(lz4ada_xxh32_state* h, const void* d_data, int64_
 	return xxh32_update_dev(h, d_data, len, static_cast<hipStream_t>(stream));
 }
 
+// XXHash32.Update over HOST bytes (lz4ada.adb:942-991) runs on the calling
+// host thread: the chain is serial, a host core runs it ~10x
+// faster than one GPU wave, and the bytes are already on the host -- a
+// device round trip per call (allocation, H2D, one-wave kernel, D2H, sync)
+// only added latency.  Device-resident bytes keep the GPU kernel
+// (lz4ada_xxh32_update_device) or the D2H pipeline (lz4ada_content_xxh32_d2h).
 int lz4ada_xxh32_update(lz4ada_xxh32_state* h, const uint8_t* data, int64_t len)
 {
 	return guarded(nullptr, [&] {
-		device_check_or_raise();
-		DevBuf<uint8_t> d;
-		d.reserve(size_t(std::max<int64_t>(len, 1)));
+		if (len < 0 || (len > 0 && !data))
+			raise(LZ4ADA_ASSERTION_ERROR, "failed precondition: XXHash32.Update input");
 		if (len > 0)
-			HIP_OK(hipMemcpy(d.p, data, size_t(len), hipMemcpyHostToDevice));
-		int st = xxh32_update_dev(h, d.p, len, nullptr);
-		if (st)
-			raise(st, g_thread_error);
+			host_xxh32_update(*h, data, size_t(len));
+		h->hash = host_xxh32_final(*h);
 	});
 }
 
-uint32_t lz4ada_xxh32_final(const lz4ada_xxh32_state* h)
-{
-	// Final() is computed on the device by every update; refresh it for a
-	// state that has not seen one yet.
-	lz4ada_xxh32_state t = *h;
-	if (t.total_length == 0 && t.hash == 0) {
-		if (xxh32_update_dev(&t, nullptr, 0, nullptr) != LZ4ADA_OK)
-			return 0;
-	}
-	return t.hash;
-}
+// XXHash32.Final (lz4ada.adb:993-1017): a pure function of the state.
+uint32_t lz4ada_xxh32_final(const lz4ada_xxh32_state* h) { return host_xxh32_final(*h); }
 
 // Content checksum pipeline: the frame-wide XXH32 is
 // one serial chain that one GPU wave runs at ~1.3 GB/s, so
@@ -1202,7 +1196,7 @@ int lz4ada_content_xxh32_d2h(lz4ada_xxh32_state* h, const void* d_data, int64_t 
 	});
 }
 
-int lz4ada_xxh32_hash(const uint8_t* data, int64_t len, uint32_t* out)
+int lz4ada_xxh32_hash(const uint8_t* data, int64_t len, uint32_t* out)  // :1019-1024
 {
 	lz4ada_xxh32_state h;
 	lz4ada_xxh32_init(&h, 0);
@@ -1820,7 +1814,7 @@ int lz4ada_launch_decode_variant(const void* d_frame, uint64_t frame_len,
                                  lz4ada_block_status* d_status, int variant, void* stream)
 {
 	return guarded(nullptr, [&] {
-		if (variant < 0 || variant > 5)
+		if (variant < 0 || variant > 6)
 			raise(LZ4ADA_ASSERTION_ERROR, "unknown decoder variant");
 		HIP_OK(launch_decode_variant(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
 		                             uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,

@@ -446,18 +446,6 @@ __device__ __forceinline__ int32_t lead_in_bytes(int32_t starts)
 	return __builtin_amdgcn_readfirstlane(min(max(l, LEAD_MIN), LEAD_MAX));
 }
 
-// Inclusive prefix maximum over the wave (values >= 0), DPP as wave_incl_scan.
-__device__ __forceinline__ int32_t wave_incl_max(int32_t v)
-{
-	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));   // row_shr:1
-	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));   // row_shr:2
-	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));   // row_shr:4
-	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));   // row_shr:8
-	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-	v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-	return v;
-}
-
 // Pass 1 of block b (the body of k_index; k_decode_idx mode 3 runs it
 // before pass 2 of the same block).
 __device__ __forceinline__ void index_block(IdxLds& X, const uint8_t* __restrict__ frame,
@@ -508,6 +496,7 @@ __device__ __forceinline__ void index_block(IdxLds& X, const uint8_t* __restrict
 	int32_t E = 0;  // exact chain entry of the current chunk
 	int32_t lead = LEAD_IN0;  // lead-in bytes (from the previous chunk's density)
 	bool bad = false;
+	bool sparse = false;  // declined as literal-heavy (k_decode_sparse takes it)
 	for (int32_t C = 0; C < n && !bad; C += CHUNK) {
 		// stage block-relative [C - mis, C - mis + CHUNK) (16-byte aligned addresses)
 #pragma unroll
@@ -610,15 +599,15 @@ __device__ __forceinline__ void index_block(IdxLds& X, const uint8_t* __restrict
 			if (s < n)
 				for (int k = 0; k < NSUB; ++k)
 					used += X.rbm[lane][k] ? 1 : 0;
-			if (__shfl(wave_incl_scan(used), 63) < CHUNK / SUB / 4)
-				bad = true;
+			if (!bad && __shfl(wave_incl_scan(used), 63) < CHUNK / SUB / 4)
+				bad = sparse = true;
 		}
 		__syncthreads();  // the next chunk overwrites the staging buffer
 	}
 	if (E != n)
 		bad = true;
 	if (lane == 0)
-		status[b].code = bad ? DS_RETRY : DS_OK;
+		status[b].code = bad ? (sparse ? DS_SPARSE : DS_RETRY) : DS_OK;
 	ISTAMP_FLUSH();
 }
 
@@ -701,11 +690,22 @@ __device__ __forceinline__ void wave_literal(g8* ob, int32_t dst, const Src& S, 
                                              int32_t len)
 {
 	const int32_t lane = int32_t(lane_id());
-	for (int32_t c = 0; c < len; c += 1024) {
-		const int32_t k = c + 16 * lane;
-		if (k < len) {
-			const u32x4 v = gload16(reinterpret_cast<uintptr_t>(S.in) + uintptr_t(src + k), S.lim);
-			gstore_n(ob + dst + k, v, min(16, len - k));
+	// 8 KiB per step, every load issued before the first store (a stored
+	// block is pure copy: one memory round trip per 8 KiB, not per 1 KiB)
+	constexpr int U = 8;
+	for (int32_t c = 0; c < len; c += 1024 * U) {
+		u32x4 v[U];
+#pragma unroll
+		for (int u = 0; u < U; ++u) {
+			const int32_t k = c + 1024 * u + 16 * lane;
+			if (k < len)
+				v[u] = gload16(reinterpret_cast<uintptr_t>(S.in) + uintptr_t(src + k), S.lim);
+		}
+#pragma unroll
+		for (int u = 0; u < U; ++u) {
+			const int32_t k = c + 1024 * u + 16 * lane;
+			if (k < len)
+				gstore_n(ob + dst + k, v[u], min(16, len - k));
 		}
 	}
 }

@@ -44,6 +44,8 @@ enum DevStatus : int32_t {
 	DS_CONTENT_SIZE = 8,   // lz4ada.adb:830-835
 	DS_INTERNAL = 9,       // decoder invariant broken (never expected)
 	DS_RETRY = 10,         // k_decode_wg declined the block: k_decode_blocks redoes it
+	DS_SPARSE = 11,        // pass 1 declined a literal-heavy block: k_decode_sparse takes it
+	                       // (k_decode_pc, retry_only, takes it like DS_RETRY)
 };
 
 // State of the serial reference-exact block kernel (emulates one
@@ -65,7 +67,7 @@ struct SerialState {
 
 // Bulk independent-block decoders (LZ4ADA_DECODE_* in lz4ada_hip.h).
 enum DecVariant : int { DEC_PC = 0, DEC_WAVE = 1, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4,
-                        DEC_IDX_LINKED = 5 };
+                        DEC_IDX_LINKED = 5, DEC_IDX_SPARSE = 6 };
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
@@ -118,6 +120,13 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                  const uint8_t* d_tab, uint8_t* d_out,
                                  lz4ada_block_status* d_status, int mode, hipStream_t stream);
+
+// Literal-heavy blocks pass 1 declined (status DS_SPARSE; lz4ada_sparse.hip):
+// decoded straight to HBM, one wave per block; anything unusual leaves the
+// block DS_RETRY for k_decode_pc.
+hipError_t launch_decode_sparse(const uint8_t* d_frame, uint64_t frame_len,
+                                const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
+                                lz4ada_block_status* d_status, hipStream_t stream);
 
 // Per-block XXH32 of the compressed payloads (block checksums).
 hipError_t launch_block_checksums(const uint8_t* d_frame,

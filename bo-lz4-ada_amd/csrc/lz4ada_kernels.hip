@@ -522,7 +522,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict_
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
 		return;
-	if (retry_only && status[b].code != DS_RETRY)
+	if (retry_only && status[b].code != DS_RETRY && status[b].code != DS_SPARSE)
 		return;
 	const int lane = int(lane_id());
 	const lz4ada_block_desc d = desc[b];
@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(128) void k_decode_pc(const uint8_t* __restrict__ f
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
 		return;
-	if (retry_only && status[b].code != DS_RETRY)
+	if (retry_only && status[b].code != DS_RETRY && status[b].code != DS_SPARSE)
 		return;
 	const int wave = int(threadIdx.x >> 6);
 	const int lane = int(lane_id());
@@ -1805,11 +1805,15 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 	}
 	if (variant == DEC_IDX_LINKED)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream, 1);
-	if (variant == DEC_IDX || variant == DEC_IDX_ALONE) {
+	if (variant == DEC_IDX || variant == DEC_IDX_ALONE || variant == DEC_IDX_SPARSE) {
 		const hipError_t err = launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out,
 		                                         d_status, stream);
 		if (err != hipSuccess || variant == DEC_IDX_ALONE)
 			return err;
+		const hipError_t e2 = launch_decode_sparse(d_frame, frame_len, d_desc, nblocks, d_out,
+		                                           d_status, stream);
+		if (e2 != hipSuccess || variant == DEC_IDX_SPARSE)
+			return e2;
 		hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
 		                   d_desc, nblocks, d_out, d_status, 1, 0);
 		return hipGetLastError();
@@ -1948,6 +1952,9 @@ hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
 	if (err == hipSuccess && !fuse)
 		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
 		                            static_cast<const uint8_t*>(tab), d_out, d_status, 0, stream);
+	// literal-heavy blocks pass 1 declined, then every other declined block
+	if (err == hipSuccess)
+		err = launch_decode_sparse(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream);
 	if (err == hipSuccess)
 		err = launch_decode_pc(d_frame, frame_len, d_desc, nblocks, d_out, d_status, 1, 0, stream);
 	const hipError_t e2 = hipFreeAsync(tab, stream);

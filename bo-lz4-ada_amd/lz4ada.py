@@ -312,7 +312,9 @@ class Decompressor:
 # ---------------------------------------------------------------- XXHash32
 
 class XXHash32:
-    """LZ4Ada.XXHash32 (lz4ada.ads:311-344); lanes advance on the GPU."""
+    """LZ4Ada.XXHash32 (lz4ada.ads:311-344).  update() hashes host bytes on the
+    host (one serial chain); update_device / update_device_d2h take
+    device-resident bytes."""
 
     def __init__(self, seed: int = 0):
         self._s = XXH32State()
@@ -431,6 +433,7 @@ def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=
 
 
 DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE, DECODE_IDX_LINKED = 0, 1, 2, 3, 4, 5
+DECODE_IDX_SPARSE = 6
 
 
 def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,
@@ -448,6 +451,7 @@ def launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stre
 
 
 DS_RETRY = 10
+DS_SPARSE = 11  # pass 1 declined a literal-heavy block (k_decode_sparse takes it)
 
 
 def launch_block_checksums(d_frame, d_descs, nblocks, d_status, stream=0):

@@ -3,7 +3,7 @@
  *
  * Drop-in boundary for the reference's public Ada API (lib/lz4ada.ads):
  * every entry point below names the reference subprogram it replaces.  An
- * Ada caller binds them with pragma Import (bindings/ada/lz4ada_hip.ads,
+ * Ada caller binds them with pragma Import (bindings/ada/lz4ada.ads,
  * INTEGRATION.md); Python binds them with ctypes (bo-lz4-ada_amd/lz4ada.py).
  *
  * Plain pointers and sizes only.  Lengths are int64_t so that both the
@@ -12,9 +12,10 @@
  * the exact Exception_Information message is available from
  * lz4ada_last_error() / lz4ada_thread_last_error().
  *
- * Block decode, block/content XXH32 and the XXHash32 API run on the GPU
- * (HIP kernels for gfx950).  Frame-header parsing and the Update state
- * machine are host code.  There is no CPU fallback: without a usable GPU,
+ * Block decode and block XXH32 run on the GPU (HIP kernels for gfx950).
+ * Frame-header parsing, the Update state machine and the serial XXH32 chain
+ * over host-resident bytes (content checksums, the XXHash32 API) are host
+ * code.  There is no CPU fallback: without a usable GPU,
  * calls that would decode return LZ4ADA_DEVICE_ERROR.
  */
 #ifndef LZ4ADA_HIP_H
@@ -112,7 +113,9 @@ void lz4ada_to_hex32(uint32_t v, char out[9]);
 /* ---------------------------------------------------------------- XXHash32 */
 
 /* LZ4Ada.XXHash32.Hasher (lz4ada.ads:335-343).  Plain struct so callers can
- * embed it; the lanes are advanced on the GPU.  `hash` caches Final(). */
+ * embed it.  Host bytes are hashed on the calling thread (the chain is one
+ * serial dependency); device-resident bytes by the GPU kernel or
+ * the D2H pipeline below, on the same state.  `hash` caches Final(). */
 typedef struct {
 	uint32_t state[4];
 	uint8_t buffer[16];
@@ -125,7 +128,8 @@ typedef struct {
 void lz4ada_xxh32_init(lz4ada_xxh32_state *h, uint32_t seed);
 /* XXHash32.Reset (lz4ada.adb:932-940). */
 void lz4ada_xxh32_reset(lz4ada_xxh32_state *h, uint32_t seed);
-/* XXHash32.Update (lz4ada.adb:942-963) over host bytes. */
+/* XXHash32.Update (lz4ada.adb:942-963) over host bytes (host chain, no
+ * device round trip). */
 int lz4ada_xxh32_update(lz4ada_xxh32_state *h, const uint8_t *data, int64_t len);
 /* Same over device-resident bytes; stream is a hipStream_t (0 = default). */
 int lz4ada_xxh32_update_device(lz4ada_xxh32_state *h, const void *d_data, int64_t len,
@@ -237,6 +241,10 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
  * earlier output as history; from the first declined or short block on,
  * every block is left with status code 10 (the exact path takes over). */
 #define LZ4ADA_DECODE_IDX_LINKED 5
+/* The index-driven decoder, then the literal-heavy decoder (k_decode_sparse)
+ * for the blocks pass 1 declines as sparse; no two-wave pass: blocks either
+ * declines keep status code 10 (retry). */
+#define LZ4ADA_DECODE_IDX_SPARSE 6
 int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                                  lz4ada_block_status *d_status, int variant, void *stream);

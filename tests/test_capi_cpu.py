@@ -210,3 +210,40 @@ def test_lz4hdrinfo(name):
     else:
         assert p.returncode == 0
         assert p.stdout.decode() == _hdrinfo_expected(data)
+
+
+# ------------------------------------------------ XXHash32 over host bytes
+# (host chain since round 3: no device needed, so these run on the CPU)
+
+def test_xxh32_kat_byte_feed():
+    """lz4test.adb:129-147: 1a x 14, 11, 10 fed one byte at a time."""
+    h = lz4ada.XXHash32()
+    for b in bytes([0x1a] * 14 + [0x11, 0x10]):
+        h.update(bytes([b]))
+    assert h.final() == 0xf994ef8a
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 15, 16, 17, 31, 32, 33, 1000, 65537])
+def test_xxh32_host_matches_oracle_and_xxhash(n):
+    import random
+    import xxhash
+    data = random.Random(n).randbytes(n)
+    want = xxhash.xxh32(data).intdigest()
+    assert O.xxh32(data) == want
+    assert lz4ada.XXHash32.hash(data) == want
+    # ragged update sizes continue one chain (Update1 / Process, lz4ada.adb:942-991)
+    h = lz4ada.XXHash32(seed=12345)  # Init ignores the seed (quirk Q1)
+    pos, step = 0, 1
+    while pos < n:
+        h.update(data[pos:pos + step])
+        pos += step
+        step = step * 3 % 37 + 1
+    assert h.final() == want
+
+
+def test_xxh32_reset_honours_seed():
+    import xxhash
+    h = lz4ada.XXHash32()
+    h.reset(7)
+    h.update(b"hello world, hello world")
+    assert h.final() == xxhash.xxh32(b"hello world, hello world", seed=7).intdigest()

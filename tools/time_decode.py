@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
-"""Decode-kernel timing for A/B experiments (no output check, so it also
-times deliberately wrong experiment builds): the bench workload of one
-class, K timed launches of the decoder selected by LZ4ADA_DECODER from the
+"""Decode-kernel timing for A/B experiments (no output check unless
+--check, so it also times deliberately wrong experiment builds): the bench
+workload of one class, K timed launches of one decoder variant from the
 library in LZ4ADA_LIB (default: the product).
 
     LZ4ADA_LIB=bo-lz4-ada_amd/_variants/liblz4ada_hip_x.so \
-        python tools/time_decode.py --kind mixed
+        python tools/time_decode.py --kind mixed --variant idx
 """
 import argparse
 import os
@@ -16,54 +16,70 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "bo-lz4-ada_amd"))
 
 import torch  # noqa: E402
+import xxhash  # noqa: E402
 
 import bench  # noqa: E402
 import lz4ada  # noqa: E402
+import lz4frame  # noqa: E402
+
+VARIANTS = {"pc": lz4ada.DECODE_PC, "wave": lz4ada.DECODE_WAVE, "wg": lz4ada.DECODE_WG,
+            "idx": lz4ada.DECODE_IDX, "idx_alone": lz4ada.DECODE_IDX_ALONE,
+            "idx_sparse": lz4ada.DECODE_IDX_SPARSE}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kind", default="mixed")
     ap.add_argument("--blocks", type=int, default=2048)
+    ap.add_argument("--unique", type=int, default=16)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--checksums", action="store_true",
-                    help="also run the block and output XXH32 kernels each step (and check them once)")
+    ap.add_argument("--variant", default="idx", help=",".join(VARIANTS) + ",product")
+    ap.add_argument("--no-bcksum", action="store_true")
+    ap.add_argument("--check", action="store_true", help="golden-check the output once")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     bmax = 4 << 20
-    recs = bench.make_unique_blocks(lz4ada.GEN_KINDS[args.kind], 64, bmax)
-    d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = bench.build_shard(recs, 0, args.blocks,
-                                                                                bmax, dev)
+    M = (lz4ada, lz4frame, xxhash, torch)
+    recs = bench.make_unique_blocks(lz4ada, lz4frame, xxhash, args.kind, args.unique, bmax,
+                                    block_cksum=not args.no_bcksum)
+    d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = bench.assemble_shard(
+        lz4ada, torch, recs, 0, args.blocks, bmax, dev)
     d_out = torch.empty(args.blocks * bmax, dtype=torch.uint8, device=dev)
     d_status = torch.zeros(args.blocks * 32, dtype=torch.uint8, device=dev)
     sh = torch.cuda.current_stream(dev).cuda_stream
     d_hash = torch.zeros(args.blocks, dtype=torch.int32, device=dev)
+    fp, dp, op, sp = d_frame.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), d_status.data_ptr()
 
-    def launch():
-        if args.checksums:
-            lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), args.blocks,
-                                          d_status.data_ptr(), sh)
-        lz4ada.launch_decode(d_frame.data_ptr(), frame_len, d_desc.data_ptr(), args.blocks,
-                             d_out.data_ptr(), d_status.data_ptr(), sh)
-        if args.checksums:
-            lz4ada.output_checksums_device(d_out.data_ptr(), d_desc.data_ptr(), d_status.data_ptr(),
-                                           args.blocks, d_hash.data_ptr(), sh)
+    for name in args.variant.split(","):
+        def launch():
+            if name == "product":
+                lz4ada.decode_blocks_device(fp, frame_len, dp, args.blocks, op, sp, sh)
+            else:
+                lz4ada.launch_decode_variant(fp, frame_len, dp, args.blocks, op, sp, VARIANTS[name],
+                                             sh)
 
-    launch()
-    torch.cuda.synchronize()
-    if args.checksums:
-        st = bench.check_statuses(d_status, args.blocks)
-        assert all(s.cksum == d.cksum for s, d in zip(st, descs)), "block checksum mismatch"
-        assert [h & 0xffffffff for h in d_hash.cpu().tolist()] == exp_hash, "output hash mismatch"
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(args.steps):
+        d_status.zero_()
         launch()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.steps
-    lib = os.path.basename(os.environ.get("LZ4ADA_LIB") or "product")
-    print(f"{lib} {args.kind} {ms:.3f} ms  {(comp + raw) / ms / 1e6:.1f} GB/s alg")
+        torch.cuda.synchronize()
+        st = bench.check_statuses(lz4ada, d_status, args.blocks)
+        codes = {}
+        for s in st:
+            codes[s.code] = codes.get(s.code, 0) + 1
+        if args.check:
+            if name != "product":
+                lz4ada.launch_block_checksums(fp, dp, args.blocks, sp, sh)
+            bench.golden_check(lz4ada, torch, d_status, descs, args.blocks, op, dp, sp, d_hash,
+                               exp_hash, sh, name)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            launch()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.steps
+        lib = os.path.basename(os.environ.get("LZ4ADA_LIB") or "product")
+        print(f"{lib} {args.kind} {name}: {ms:.3f} ms  {(comp + raw) / ms / 1e6:.1f} GB/s alg "
+              f"frac {(comp + raw) / ms / 1e6 / 8000:.4f}  codes {codes}", flush=True)
 
 
 if __name__ == "__main__":
