@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			uintptr_t a = g + 1024u * r;
 			if (a + 16 > lim)
 				a = (lim - 16) & ~uintptr_t(15);
-			const uint32_t l = ring_lds + uint32_t(c % NSLOT) * STG + 1024u * r;
+			const uint32_t l = uni(ring_lds + uint32_t(c % NSLOT) * STG + 1024u * r);
 			uint32_t m0save;
 			asm volatile(
 			    "s_mov_b32 %0, m0\n\t"
@@ -296,6 +296,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	int32_t shi = 0;  // = landed * STG: bytes below it (from abase) are in LDS
 	// make block-relative bytes [.., pend) readable (pend wave-uniform)
 	auto ensure = [&](int32_t pend) {
+		pend = int32_t(uni(uint32_t(pend)));  // wave-uniform: scalar control and DMA operands
 		const int32_t need = (pend + mis - 1) / STG;  // last chunk needed
 		if (need >= issued) {
 			// a long literal run jumped past the chunks in flight: settle them
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	// 8 bytes at block-relative pos, already readable.  pos is wave-uniform,
 	// and so is the parse on it (scalar unit).
 	auto lds8 = [&](int32_t pos, uint32_t& lo, uint32_t& hi) {
-		const uint32_t a = uint32_t(pos + mis);
+		const uint32_t a = uni(uint32_t(pos + mis));
 		const uint32_t r0 = a & ~3u;
 		const uint32_t* w = reinterpret_cast<const uint32_t*>(S.ring);
 		const uint32_t w0 = w[(r0 & (RING - 1)) >> 2], w1 = w[((r0 + 4) & (RING - 1)) >> 2],
@@ -329,7 +330,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 		lo = uni(__builtin_amdgcn_alignbyte(w1, w0, sh));
 		hi = uni(__builtin_amdgcn_alignbyte(w2, w1, sh));
 	};
+	// the same into VGPRs (the fast parse path below stays on the VALU)
+	auto lds8v = [&](int32_t pos, uint32_t& lo, uint32_t& hi) {
+		const uint32_t a = uint32_t(pos + mis);
+		const uint32_t r0 = a & ~3u;
+		const uint32_t* w = reinterpret_cast<const uint32_t*>(S.ring);
+		const uint32_t w0 = w[(r0 & (RING - 1)) >> 2], w1 = w[((r0 + 4) & (RING - 1)) >> 2],
+		               w2 = w[((r0 + 8) & (RING - 1)) >> 2];
+		const uint32_t sh = a & 3u;
+		lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+		hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+		asm volatile("" : "+v"(lo), "+v"(hi));
+	};
 	auto rd8 = [&](int32_t pos, uint32_t& lo, uint32_t& hi) {
+		pos = int32_t(uni(uint32_t(pos)));
 		if (pos + mis + 8 > shi)
 			ensure(pos + 8);
 		lds8(pos, lo, hi);
@@ -370,102 +384,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 		// sequence j of the batch lands in lane j
 		int32_t r_lit = 0, r_L = 0, r_dst = 0, r_off = 0, r_ml = 0;
 		int32_t ns = 0, pieces = 0;
-		while (ns < NSEQ) {
-			if (p >= n) {
-				done = true;  // the chain ended right after a match
-				break;
-			}
-			// bytes up to p + 1100 readable: the token's window and, for the
-			// common shape (L <= 15 + 4 x 255), the offset read
-			if (p + mis + 1100 > shi)
-				ensure(p + 1100);
-			// the common shape, with few branches: the literal length's
-			// extension bytes inside the token's window (>= 4 of them), at most
-			// one match-length extension byte, not the last sequence, well formed
-			const uint64_t tw = uint64_t(t0) | (uint64_t(t1) << 32);
-			const uint32_t tk = t0 & 0xffu;
-			int32_t L = int32_t(tk >> 4);
-			int32_t lit = p + 1;
-			bool ok = tv >= 5;
-			if (L == 15) {
-				// first extension byte != 0xFF among the window's tv - 1
-				const uint64_t nf = ~(tw >> 8) & ((uint64_t(1) << (8 * (tv - 1))) - 1);
-				const int32_t k = int32_t(__builtin_ctzll(nf | (uint64_t(1) << 63))) >> 3;
-				ok = ok && nf != 0;
-				L += 255 * k + int32_t((tw >> (8 * k + 8)) & 0xffu);
-				lit += k + 1;
-			}
-			int32_t x = lit + L;
-			ok = ok && x + 1 < n && L <= 15 + 4 * 255;
-			uint32_t w0 = 0, w1 = 0;
-			if (ok)
-				lds8(x, w0, w1);  // offset, match-length byte, the next token
-			int32_t off = int32_t(w0 & 0xffffu);
-			int32_t M = int32_t(tk & 15u);
-			const uint32_t e = (w0 >> 16) & 0xffu;
-			const bool x2 = M == 15;
-			int32_t ml = M + 4 + (x2 ? int32_t(e) : 0);
-			int32_t next = x + 2 + (x2 ? 1 : 0);
-			ok = ok && !(x2 && e == 255u) && off != 0 && off <= o + L && o + L + ml <= cap;
-			if (__builtin_expect(ok, 1)) {
-				const int32_t used = next - x;  // 2 or 3: the next token is in w
-				t0 = __builtin_amdgcn_alignbyte(w1, w0, uint32_t(used));
-				t1 = w1 >> (8 * used);
-				tv = 8 - used;
-			} else {
-				// every other shape, the general way (rare)
-				rd8(p, t0, t1);
-				const uint32_t tk2 = t0 & 0xffu;
-				tv = 0;
-				L = int32_t(tk2 >> 4);
-				lit = p + 1;
-				if (L == 15) {
-					lit = ext_slow(p + 1, L);
-					if (lit < 0) {
-						bad = true;
-						break;
-					}
-				}
-				x = lit + L;
-				M = int32_t(tk2 & 15u);
-				off = 0;
-				ml = 0;
-				next = n;
-				if (x >= n) {
-					// the block's last sequence: literals only (:748-764)
-					if (x > n || M != 0 || o + L > cap) {
-						bad = true;
-						break;
-					}
-					done = true;
-				} else {
-					if (x + 1 >= n) {
-						bad = true;
-						break;
-					}
-					rd8(x, w0, w1);
-					off = int32_t(w0 & 0xffffu);
-					next = x + 2;
-					if (M == 15) {
-						next = ext_slow(x + 2, M);
-						if (next < 0) {
-							bad = true;
-							break;
-						}
-					}
-					ml = M + 4;
-					// off 0, a reference before the block start (D2) or a slot
-					// overflow: k_decode_pc gives the exact status
-					if (off == 0 || off > o + L || int64_t(o) + L + ml > cap) {
-						bad = true;
-						break;
-					}
-				}
-				if (!done) {
-					rd8(next, t0, t1);  // the next token's window
-					tv = 8;
-				}
-			}
+		auto record = [&](int32_t lit, int32_t L, int32_t off, int32_t ml) {
 			const bool mine = lane == ns;
 			r_lit = mine ? lit : r_lit;
 			r_L = mine ? L : r_L;
@@ -474,10 +393,105 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			r_ml = mine ? ml : r_ml;
 			pieces += L > BIG ? 0 : (L + 15) >> 4;
 			o += L + ml;
-			p = next;
 			++ns;
-			if (done || pieces > OWN - BIG / 16)
+		};
+		for (;;) {
+			// -- the common shape, a tight scalar loop (the CU's eight waves
+			// share one scalar unit, so instructions per sequence are the
+			// cost): the literal length's extension bytes among the token
+			// window's bytes 1..4, at most one match-length extension byte, not
+			// the last sequence, well formed, the offset within the staged
+			// bytes.  Anything else leaves it for the general code below.
+			while (ns < NSEQ && pieces <= OWN - BIG / 16 && tv >= 5 && p + mis + 1100 <= shi) {
+				const uint32_t tk = t0 & 0xffu;
+				const uint32_t ex = uint32_t((uint64_t(t0) | (uint64_t(t1) << 32)) >> 8);  // bytes 1..4
+				const uint32_t kb = uint32_t(__builtin_ctz(~ex | 0x80000000u)) & ~7u;  // 8 x first non-0xFF
+				const bool isx = tk >= 0xf0u;
+				const int32_t L = isx ? int32_t(15 + 255 * (kb >> 3) + ((ex >> kb) & 0xffu)) : int32_t(tk >> 4);
+				const int32_t lit = p + 1 + (isx ? int32_t(kb >> 3) + 1 : 0);
+				const int32_t x = lit + L;
+				if ((isx && (~ex) == 0u) || x + 1 >= n)
+					break;
+				uint32_t w0, w1;
+				lds8(x, w0, w1);  // offset, match-length byte, the next token
+				const int32_t off = int32_t(w0 & 0xffffu);
+				const int32_t M = int32_t(tk & 15u);
+				const uint32_t e = (w0 >> 16) & 0xffu;
+				const bool x2 = M == 15;
+				const int32_t ml = M + 4 + (x2 ? int32_t(e) : 0);
+				if ((x2 && e == 255u) || off == 0 || off > o + L || o + L + ml > cap)
+					break;
+				const int32_t used = x2 ? 3 : 2;  // the next token is in w
+				const uint64_t w = (uint64_t(w0) | (uint64_t(w1) << 32)) >> (8 * used);
+				t0 = uint32_t(w);
+				t1 = uint32_t(w >> 32);
+				tv = 8 - used;
+				record(lit, L, off, ml);
+				p = x + used;
+			}
+			if (ns >= NSEQ || pieces > OWN - BIG / 16)
 				break;
+			if (p >= n) {
+				done = true;  // the chain ended right after a match
+				break;
+			}
+			if (p + mis + 1100 > shi) {
+				ensure(p + 1100);
+				if (tv >= 5)
+					continue;
+			}
+			// -- one sequence, the general way (rare)
+			rd8(p, t0, t1);
+			tv = 8;
+			const uint32_t tk = t0 & 0xffu;
+			int32_t L = int32_t(tk >> 4);
+			int32_t lit = p + 1;
+			if (L == 15) {
+				lit = ext_slow(p + 1, L);
+				if (lit < 0) {
+					bad = true;
+					break;
+				}
+			}
+			const int32_t x = lit + L;
+			int32_t M = int32_t(tk & 15u), off = 0, ml = 0, next = n;
+			if (x >= n) {
+				// the block's last sequence: literals only (:748-764)
+				if (x > n || M != 0 || o + L > cap) {
+					bad = true;
+					break;
+				}
+				done = true;
+			} else {
+				if (x + 1 >= n) {
+					bad = true;
+					break;
+				}
+				uint32_t w0, w1;
+				rd8(x, w0, w1);
+				off = int32_t(w0 & 0xffffu);
+				next = x + 2;
+				if (M == 15) {
+					next = ext_slow(x + 2, M);
+					if (next < 0) {
+						bad = true;
+						break;
+					}
+				}
+				ml = M + 4;
+				// off 0, a reference before the block start (D2) or a slot
+				// overflow: k_decode_pc gives the exact status
+				if (off == 0 || off > o + L || int64_t(o) + L + ml > cap) {
+					bad = true;
+					break;
+				}
+			}
+			record(lit, L, off, ml);
+			p = next;
+			if (done)
+				break;
+			rd8(p, t0, t1);  // the next token's window
+			tv = 8;
 		}
 		nseq += ns;
 		if (bad || ns == 0)
