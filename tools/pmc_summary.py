@@ -23,7 +23,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_decode_idx", "k_index", "k_decode_pc", "k_decode_wg", "k_decode_blocks",
+KERNELS = ("k_decode_idx", "k_index", "k_decode_sparse", "k_decode_pc", "k_decode_wg", "k_decode_blocks",
            "k_xxh32_rows", "k_serial_block", "k_xxh32_update",
            "k_compact")
 
@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--kind", default="mixed")
     ap.add_argument("--blocks", type=int, default=2048)
     ap.add_argument("--block-max", type=int, default=4 << 20)
+    ap.add_argument("--first", type=int, default=0,
+                    help="only the first N dispatches of each kernel (the bench's headline "
+                         "workload runs first: warmup + steps)")
     args = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -55,13 +58,40 @@ def main():
             if k:
                 avg_ns[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
 
+    # per-dispatch durations from the kernel trace (the --stats average mixes
+    # every workload the command runs; --first keeps the headline's)
+    trace = os.path.join(args.dir, "trace", "run_kernel_trace.csv")
+    if args.first and os.path.exists(trace):
+        durs = collections.defaultdict(list)
+        with open(trace) as fh:
+            rows = sorted(csv.DictReader(fh), key=lambda r: int(r["Dispatch_Id"]))
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            if k:
+                durs[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        for k, v in durs.items():
+            v = v[:args.first]
+            avg_ns[k] = {"calls": len(v), "avg_ns": sum(v) / len(v), "first_dispatches": args.first}
+        # the headline's dispatches, one row each (the --stats average mixes workloads)
+        with open(os.path.join(prof, f"{args.tag}_headline_dispatches.csv"), "w") as fh:
+            fh.write("kernel,dispatch_index,duration_ns\n")
+            for k, v in sorted(durs.items()):
+                for i, ns in enumerate(v[:args.first]):
+                    fh.write(f"{k},{i},{ns}\n")
+
     counters = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(args.dir, "pmc*", "run_counter_collection.csv"))):
         with open(f) as fh:
-            for r in csv.DictReader(fh):
-                k = short(r["Kernel_Name"])
-                if k:
-                    counters[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            rows = list(csv.DictReader(fh))
+        seen = collections.defaultdict(list)  # kernel -> dispatch ids in order
+        for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+            k = short(r["Kernel_Name"])
+            if k and int(r["Dispatch_Id"]) not in seen[k]:
+                seen[k].append(int(r["Dispatch_Id"]))
+        for r in rows:
+            k = short(r["Kernel_Name"])
+            if k and (not args.first or int(r["Dispatch_Id"]) in seen[k][:args.first]):
+                counters[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     per = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in counters.items()}
 
     out = {"tag": args.tag, "kernels": {}}
@@ -88,7 +118,7 @@ def main():
         json.dump(out, fh, indent=1)
 
     ks = out["kernels"]
-    if "k_decode_idx" in ks and "k_index" in ks:
+    if "k_decode_idx" in ks and "k_index" in ks and not args.first:
         # the default decode path is two kernels: report their sum per launch
         a, b = ks["k_index"], ks["k_decode_idx"]
         dname = "k_index+k_decode_idx"

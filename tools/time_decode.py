@@ -54,6 +54,8 @@ def main():
         def launch():
             if name == "product":
                 lz4ada.decode_blocks_device(fp, frame_len, dp, args.blocks, op, sp, sh)
+            elif name == "cksum":
+                lz4ada.launch_block_checksums(fp, dp, args.blocks, sp, sh)
             else:
                 lz4ada.launch_decode_variant(fp, frame_len, dp, args.blocks, op, sp, VARIANTS[name],
                                              sh)
@@ -65,7 +67,10 @@ def main():
         codes = {}
         for s in st:
             codes[s.code] = codes.get(s.code, 0) + 1
-        if args.check:
+        if args.check and name == "cksum":
+            bad = [i for i in range(args.blocks) if st[i].cksum != descs[i].cksum]
+            assert not bad, f"block checksum mismatch {bad[:5]}"
+        elif args.check:
             if name != "product":
                 lz4ada.launch_block_checksums(fp, dp, args.blocks, sp, sh)
             bench.golden_check(lz4ada, torch, d_status, descs, args.blocks, op, dp, sp, d_hash,
