@@ -290,9 +290,18 @@ def bench_class(M, dev, sh, stream, cls, nb, bmax, block_cksum=True, unique=16):
         b.record(stream)
     torch.cuda.synchronize()
     ms = sum(a.elapsed_time(b) for a, b in ev) / reps
+    # the decoder alone (no block checksums beside it)
+    for a, b in ev:
+        a.record(stream)
+        lz4ada.launch_decode(fp, fl, dp, nb, op, sp, sh)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms_dec = sum(a.elapsed_time(b) for a, b in ev) / reps
     flg = 0x60 | (0x10 if block_cksum else 0)
     row = {"decode_ms": round(ms, 3), "MiB_s": round(rb / (ms * 1e-3) / MiB, 1),
            "frac": round((cb + rb) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "decoder_alone_ms": round(ms_dec, 3),
+           "decoder_alone_frac": round((cb + rb) / (ms_dec * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
            "ratio": round(cb / rb, 4), "flg": f"0x{flg:02x}", "blocks": nb,
            "compressed_bytes": cb, "decoded_bytes": rb,
            "golden": "per-block XXH32 of the output vs the generator"}
@@ -630,6 +639,7 @@ def main():
         del d_out
         rows = {}
         for cls in [c for c in args.classes.split(",") if c]:
+            log(f"[bench] class {cls} ...")
             if cls == "stored":
                 # README.md:753-766's `random` rows: lz4 CLI defaults, no block checksum
                 rows["stored"] = bench_class(M, dev, sh, stream, "stored", nb, bmax, block_cksum=False)
@@ -642,12 +652,15 @@ def main():
     # ---- configs[4]: linked (dependent) 256 KiB-block frame, 1 GiB, one GPU:
     # every block at once against synthetic history, resolved on the GPU
     if extra and not args.no_linked:
+        log("[bench] configs[4] linked row ...")
         result["linked_c5"] = bench_linked(M, dev, sh, stream)
     # ---- configs[1]: 1 GiB of 64 KiB independent blocks + content checksum
     if extra and not args.no_64k:
+        log("[bench] configs[1] 64 KiB row ...")
         result["c2_64k"] = bench_64k(M, dev, sh, stream)
 
     if extra and not args.no_cpu_baseline:
+        log("[bench] CPU baseline (oracle) ...")
         result["cpu_baseline"] = cpu_baseline(lz4frame, xxhash, recs, bmax, args.cpu_budget)
         threads = min(16, os.cpu_count() or 1)
         result["cpu_baseline_parallel"] = cpu_baseline_parallel(lz4frame, xxhash, recs, bmax,

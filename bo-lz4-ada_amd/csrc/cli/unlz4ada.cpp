@@ -1,10 +1,12 @@
 // unlz4ada -- counterpart of the reference CLI (tool_unlz4ada/unlz4ada.adb):
 // decompress every frame of stdin (or of the file named by argv[1]) to
 // stdout.  Frames go through the library's bulk GPU path one at a time
-// (lz4ada_decode_frame_alloc: Init_With_Header(Single_Frame) + Update
+// (lz4ada_decode_frame_partial: Init_With_Header(Single_Frame) + Update
 // semantics per frame, as the reference tool re-inits per frame,
 // unlz4ada.adb:84-87); each frame's bytes are written before the next
-// frame is decoded.  An error prints the reference's Exception_Information
+// frame is decoded, and a failing frame's blocks before the failing block
+// are written before the error, as the reference's per-block writes leave
+// them.  An error prints the reference's Exception_Information
 // line ("raised LZ4ADA.<NAME> : <message>") to stderr and exits 1; fewer
 // than 7 bytes left at a frame start is the tool's own
 // "Partial frame detected" Constraint_Error (unlz4ada.adb:65-76).
@@ -47,11 +49,15 @@ int main(int argc, char** argv)
 			return fail(LZ4ADA_CONSTRAINT_ERROR, "Partial frame detected. Unable to process all data");
 		uint8_t* out = nullptr;
 		int64_t out_len = 0, consumed = 0;
-		const int st = lz4ada_decode_frame_alloc(in.data() + pos, len - pos, &out, &out_len, &consumed);
-		if (st != LZ4ADA_OK)
-			return fail(st, lz4ada_thread_last_error());
+		// on an error, the blocks the reference wrote before raising come
+		// back too (unlz4ada.adb:41 writes each block as Update returns it)
+		const int st = lz4ada_decode_frame_partial(in.data() + pos, len - pos, &out, &out_len, &consumed);
 		const bool ok = out_len == 0 || fwrite(out, 1, size_t(out_len), stdout) == size_t(out_len);
 		lz4ada_buffer_free(out);
+		if (st != LZ4ADA_OK) {
+			fflush(stdout);
+			return fail(st, lz4ada_thread_last_error());
+		}
 		if (!ok) {
 			perror("stdout");
 			return 2;

@@ -395,6 +395,10 @@ struct lz4ada_decompressor {
 
 	// device side (lazily created at the first block)
 	bool dev_ready = false;
+	// check the next block's checksum before launching the speculative
+	// decode (the block a bulk path stopped at: a decode of a corrupted
+	// payload may be long, and would have to finish before the raise)
+	bool checksum_first = false;
 	int device = -1;
 	hipStream_t stream = nullptr;
 	DevBuf<uint8_t> d_buf;  // mirror of the caller's Buffer (history lives here)
@@ -614,6 +618,16 @@ struct lz4ada_decompressor {
 			HIP_OK(hipEventRecord(ev_in, stream));
 			HIP_OK(hipStreamWaitEvent(side, ev_in, 0));
 			HIP_OK(launch_xxh32_update(d_tmp_hash.p, d_blk.p, uint64_t(raw_len), side));
+		}
+		if (checksum_first && bcl > 0) {
+			checksum_first = false;
+			HIP_OK(hipMemcpyAsync(&h, d_tmp_hash.p, sizeof h, hipMemcpyDeviceToHost, side));
+			HIP_OK(hipStreamSynchronize(side));
+			const uint32_t expect = load32(blk + blen - bcl);
+			if (h.hash != expect)
+				raise(LZ4ADA_CHECKSUM_ERROR, "Declared checksum is 0x" + hex32(expect) +
+				                                     ", but computed one is 0x" + hex32(h.hash) +
+				                                     ".");
 		}
 		const int64_t fast_start = launch_fast_block(raw_len, blen, buflen);
 		if (bcl > 0) {
@@ -1327,9 +1341,55 @@ struct Sink {
 	void commit(int64_t n) { len += n; }
 };
 
+// Where the exact path resumes a frame the bulk path decoded up to a failing
+// block: the stream state Decode_Full_Block_With_Trailer would have there
+// (lz4ada.adb:661-714) -- Output_Pos / Output_Pos_History replayed from the
+// decoded lengths (:678-690, 785-787), the content size left (:826-839) and
+// the content hash (:709-714) over the bytes already committed.
+struct Resume {
+	int64_t at = 0;          // frame offset of the resume block's size word
+	int64_t output_pos = 0;  // Ctx.Output_Pos before it
+	int64_t output_pos_history = 0;
+	uint64_t committed = 0;  // bytes of the blocks before it
+	lz4ada_xxh32_state hash{};
+	const uint8_t* output = nullptr;  // those bytes, and each block's length
+	const std::vector<uint32_t>* lens = nullptr;
+	bool checksum_first = false;  // check the resume block's checksum before decoding it
+};
+
+// The reference's Buffer as it stands before the resume block: blocks form
+// "rounds" -- one starts at Buffer position 0 whenever Output_Pos has
+// reached 64 KiB (lz4ada.adb:678-680) and appends otherwise -- so Buffer(x)
+// holds byte x of the newest round longer than x (zero if none is).
+static void buffer_image(const Resume& rs, uint8_t* img, int64_t size)
+{
+	memset(img, 0, size_t(size));
+	const auto& lens = *rs.lens;
+	std::vector<std::pair<int64_t, int64_t>> rounds;  // (output offset, length)
+	int64_t pos = 0, off = 0;
+	for (size_t j = 0; j < lens.size(); ++j) {
+		if (rounds.empty() || pos >= HISTORY_SIZE) {
+			rounds.emplace_back(off, 0);
+			pos = 0;
+		}
+		pos += lens[j];
+		off += lens[j];
+		rounds.back().second = pos;
+	}
+	int64_t filled = 0;
+	for (size_t r = rounds.size(); r-- > 0 && filled < size;) {
+		const int64_t hi = std::min(rounds[r].second, size);
+		if (hi > filled)
+			memcpy(img + filled, rs.output + rounds[r].first + filled, size_t(hi - filled));
+		filled = std::max(filled, hi);
+	}
+}
+
 // Reference-exact path for one frame: the unlz4ada loop
-// (tool_unlz4ada/unlz4ada.adb:84-103) over the streaming engine.
-static void exact_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& consumed_total)
+// (tool_unlz4ada/unlz4ada.adb:84-103) over the streaming engine, from the
+// frame start or from `resume`.
+static void exact_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& consumed_total,
+                        const Resume* resume = nullptr)
 {
 	int64_t consumed = 0, mbs = 0;
 	lz4ada_decompressor* raw = nullptr;
@@ -1340,6 +1400,23 @@ static void exact_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& consu
 	std::vector<uint8_t> buf(size_t(mbs), 0);
 	int eof = LZ4ADA_EOF_NO;
 	int64_t pos = consumed;
+	if (resume) {
+		ctx->output_pos = resume->output_pos;
+		ctx->output_pos_history = resume->output_pos_history;
+		if (ctx->m.has_content_size)
+			ctx->m.size_remaining -= resume->committed;
+		ctx->hash_all = resume->hash;
+		ctx->checksum_first = resume->checksum_first;
+		pos = resume->at;
+		if (resume->lens && !resume->lens->empty()) {
+			// the history the resume block may read: Buffer and its mirror
+			buffer_image(*resume, buf.data(), int64_t(buf.size()));
+			ctx->ensure_device();
+			if (ctx->d_buf_len < int64_t(buf.size()))
+				ctx->grow_mirror(int64_t(buf.size()));
+			HIP_OK(hipMemcpy(ctx->d_buf.p, buf.data(), buf.size(), hipMemcpyHostToDevice));
+		}
+	}
 	while (pos < len) {
 		int64_t c = 0, first = 1, last = 0;
 		ctx->update(f + pos, len - pos, c, buf.data(), mbs, first, last);
@@ -1451,15 +1528,21 @@ static std::vector<std::pair<uint32_t, uint32_t>> batches_of(const std::vector<l
 	return v;
 }
 
-enum BulkResult { BULK_OK, BULK_EXACT, BULK_PRE_REF };
+enum BulkResult { BULK_OK, BULK_EXACT, BULK_PRE_REF, BULK_FAIL_AT };
 
 // Independent blocks, batch by batch: block checksums + the bulk decoder
 // over slots, then the batch's bytes (compacted if a block is short) to the
 // sink, hashed on the way when the frame has a content checksum.
+// BULK_FAIL_AT: block `fail` has a bad status or checksum; the blocks before
+// it are committed (their lengths in `lens`), so the exact path can resume
+// there instead of redoing the frame.
 static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_info& info,
                                    const std::vector<lz4ada_block_desc>& descs, Sink& out,
-                                   lz4ada_xxh32_state* h, uint64_t& total)
+                                   lz4ada_xxh32_state* h, uint64_t& total,
+                                   std::vector<uint32_t>& lens, int64_t& fail)
 {
+	lens.clear();
+	fail = -1;
 	hipStream_t stream = nullptr;
 	uint64_t budget = uint64_t(env_bytes("LZ4ADA_BATCH_BYTES", int64_t(4) << 30));
 	uint32_t lo = 0;
@@ -1468,7 +1551,7 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 		const auto bt = batches_of(std::vector<lz4ada_block_desc>(descs.begin() + lo, descs.end()),
 		                           info.block_max, 0, budget);
 		const uint32_t hi = lo + bt[0].second;
-		const uint32_t nb = hi - lo;
+		uint32_t nb = hi - lo;
 		std::vector<lz4ada_block_desc> d(descs.begin() + lo, descs.begin() + hi);
 		uint64_t slots = 0;
 		for (auto& x : d) {
@@ -1494,26 +1577,29 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 		                             stream));
 		std::vector<lz4ada_block_status> st(nb);
 		HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status), hipMemcpyDeviceToHost));
-		bool pre = false;
 		uint64_t bt_total = 0;
 		bool contiguous = true;
 		std::vector<uint64_t> dst_off(nb);
+		uint32_t ok_n = nb;  // the blocks before the first failing one
 		for (uint32_t i = 0; i < nb; ++i) {
-			if (st[i].code == DS_PRE_BLOCK_REF) {
-				pre = true;  // B.Indep set, but the block reads earlier blocks (D2)
-				continue;
+			// the block checksum is checked before decoding (lz4ada.adb:672-676)
+			if ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum) {
+				ok_n = i;
+				break;
 			}
-			if (st[i].code != DS_OK)
-				return BULK_EXACT;
-			if ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum)
-				return BULK_EXACT;
+			if (st[i].code == DS_PRE_BLOCK_REF)
+				return BULK_PRE_REF;  // B.Indep set, but the block reads earlier blocks (D2)
+			if (st[i].code != DS_OK) {
+				ok_n = i;
+				break;
+			}
 			dst_off[i] = bt_total;
 			if (bt_total != d[i].out_off)
 				contiguous = false;
 			bt_total += st[i].out_len;
 		}
-		if (pre)
-			return BULK_PRE_REF;
+		const uint32_t nb_all = nb;
+		nb = ok_n;
 		const uint8_t* d_res = d_out;
 		if (!contiguous) {
 			DevBuf<uint64_t> d_off;
@@ -1533,6 +1619,12 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 			HIP_OK(hipMemcpy(dst, d_res, size_t(bt_total), hipMemcpyDeviceToHost));
 		out.commit(int64_t(bt_total));
 		total += bt_total;
+		for (uint32_t i = 0; i < nb; ++i)
+			lens.push_back(st[i].out_len);
+		if (nb < nb_all) {
+			fail = int64_t(lo) + nb;
+			return BULK_FAIL_AT;
+		}
 		lo = hi;
 	}
 	return BULK_OK;
@@ -1560,8 +1652,11 @@ static void d2h(void* dst, const void* src, size_t n, hipStream_t stream)
 // the frame start, no device memory).
 static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block_max,
                               const std::vector<lz4ada_block_desc>& descs, LinkedSink& sink,
-                              uint64_t& total, hipStream_t stream)
+                              uint64_t& total, std::vector<uint32_t>& lens, int64_t& fail,
+                              hipStream_t stream)
 {
+	lens.clear();
+	fail = -1;
 	// a batch holds 3 decode buffers (slots + 64 KiB regions) and one 4-byte
 	// word per output byte: ~7x its slot bytes
 	uint64_t budget = uint64_t(env_bytes("LZ4ADA_LINKED_BATCH_BYTES", int64_t(2) << 30));
@@ -1591,7 +1686,7 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		const auto bt = batches_of(std::vector<lz4ada_block_desc>(descs.begin() + lo, descs.end()),
 		                           block_max, uint64_t(HISTORY_SIZE), budget);
 		const uint32_t hi = lo + bt[0].second;
-		const uint32_t nb = hi - lo;
+		uint32_t nb = hi - lo;
 		std::vector<lz4ada_block_desc> d(descs.begin() + lo, descs.begin() + hi);
 		uint64_t bytes = 0;
 		for (auto& x : d) {
@@ -1640,22 +1735,32 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		d2h(st.data(), sx.p, sb, stream);
 		std::vector<int64_t> A(nb);
 		int64_t n = 0;
+		// the first block the exact path has to take: a block error, a
+		// checksum mismatch, or quirk D1 (a match reaching
+		// >= D1_OFF back into the history right after a block that ended at
+		// 65536..65542).  The blocks before it only point backwards, so they
+		// resolve on their own and the exact path resumes at it.
+		uint32_t ok_n = nb;
 		for (uint32_t i = 0; i < nb; ++i) {
-			if (st[i].code != DS_OK)
-				return BULK_EXACT;
-			if ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum)
-				return BULK_EXACT;
-			// D1: a match reaching >= D1_OFF back into
-			// the history right after a block that ended at 65536..65542
 			if (opos >= HISTORY_SIZE)
 				opos = 0;
-			if ((st[i].aux & AUX_D1_RISK) && oph >= HISTORY_SIZE && oph <= HISTORY_SIZE + 6)
-				return BULK_EXACT;
+			if (st[i].code != DS_OK ||
+			    ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum) ||
+			    ((st[i].aux & AUX_D1_RISK) && oph >= HISTORY_SIZE && oph <= HISTORY_SIZE + 6)) {
+				ok_n = i;
+				break;
+			}
 			opos += st[i].out_len;
 			if (opos >= HISTORY_SIZE)
 				oph = opos;
 			A[i] = n;
 			n += st[i].out_len;
+		}
+		if (ok_n < nb) {
+			fail = int64_t(lo) + ok_n;
+			nb = ok_n;
+			if (nb == 0)
+				return BULK_FAIL_AT;
 		}
 		if (n >= (int64_t(1) << 31) - HISTORY_SIZE) {  // words hold positions + 65536 in 31 bits
 			if (nb > 1) {
@@ -1701,6 +1806,10 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		sink.done(F, n);
 		phase("sink");
 		total += uint64_t(n);
+		for (uint32_t i = 0; i < nb; ++i)
+			lens.push_back(st[i].out_len);
+		if (fail >= 0)
+			return BULK_FAIL_AT;
 		lo = hi;
 	}
 	return BULK_OK;
@@ -1709,6 +1818,23 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 // Which paths the last lz4ada_decode_* call on this thread took
 // (LZ4ADA_PATH_* bits; tests and diagnostics).
 static thread_local int g_last_path = 0;
+
+// The stream state before block `fail`, the first one the bulk path could
+// not take (its predecessors are committed): Output_Pos and
+// Output_Pos_History as lz4ada.adb:678-690 and 785-787 leave them.
+static void resume_state(const std::vector<uint32_t>& lens, Resume& rs)
+{
+	int64_t pos = 0, oph = 0;
+	for (uint32_t n : lens) {
+		if (pos >= HISTORY_SIZE)  // :678-680
+			pos = 0;
+		pos += n;
+		if (pos >= HISTORY_SIZE)  // :688-690, 785-787
+			oph = pos;
+	}
+	rs.output_pos = pos;
+	rs.output_pos_history = oph;
+}
 
 // One frame from host memory (Single_Frame semantics): the bulk path when
 // the frame indexes cleanly, else -- or when the bulk path finds anything
@@ -1729,14 +1855,28 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 		return;
 	}
 	const int64_t base = out.len;
+	// LZ4ADA_TRACE_FRAME=1: phase times (synchronised) to stderr
+	static const bool trace = getenv("LZ4ADA_TRACE_FRAME") != nullptr;
+	auto t0 = std::chrono::steady_clock::now();
+	auto phase = [&](const char* name) {
+		if (!trace)
+			return;
+		HIP_OK(hipDeviceSynchronize());
+		const auto t1 = std::chrono::steady_clock::now();
+		fprintf(stderr, "[frame] %-10s %8.3f ms\n", name,
+		        std::chrono::duration<double, std::milli>(t1 - t0).count());
+		t0 = t1;
+	};
 	if (indexed && info.frame_len <= len && info.format != LZ4ADA_FORMAT_SKIPPABLE &&
 	    !getenv("LZ4ADA_EXACT_ONLY")) {
 		device_check_or_raise();
 		struct {
 			uint8_t* p;
 		} d_frame{ scratch(SC_FRAME, size_t(info.frame_len)) };
+		phase("index");
 		if (d_frame.p) {
 			HIP_OK(hipMemcpy(d_frame.p, f, size_t(info.frame_len), hipMemcpyHostToDevice));
+			phase("h2d");
 			lz4ada_xxh32_state hs;
 			lz4ada_xxh32_reset(&hs, 0);
 			lz4ada_xxh32_state* h = info.content_checksum ? &hs : nullptr;
@@ -1744,8 +1884,11 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 			// the reference decodes every frame as linked (B.Indep is never
 			// read, lz4ada.adb:267-275); independent blocks are the fast case
 			BulkResult r = BULK_PRE_REF;
+			std::vector<uint32_t> lens;
+			int64_t fail = -1;
 			if (info.independent && !getenv("LZ4ADA_FORCE_LINKED"))
-				r = bulk_independent(d_frame.p, info, descs, out, h, total);
+				r = bulk_independent(d_frame.p, info, descs, out, h, total, lens, fail);
+			phase("bulk");
 			const bool linked = r == BULK_PRE_REF;
 			if (linked) {
 				out.len = base;
@@ -1763,7 +1906,32 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 					out.commit(n);
 				};
 				r = bulk_linked(d_frame.p, uint64_t(info.frame_len), info.block_max, descs, ls, total,
-				                nullptr);
+				                lens, fail, nullptr);
+			}
+			if (r == BULK_FAIL_AT && !getenv("LZ4ADA_NO_RESUME")) {
+				// the reference outputs blocks 0 .. fail-1 and then raises in
+				// block `fail` (lz4ada.adb:672-676: each block is checked when it
+				// is reached): the exact path resumes at that block, over the
+				// Buffer the committed blocks leave, not at byte 0
+				Resume rs;
+				resume_state(lens, rs);
+				rs.committed = total;
+				rs.hash = hs;  // the blocks before `fail`, hashed on their way out
+				rs.output = out.p + base;
+				rs.lens = &lens;
+				rs.at = int64_t(descs[size_t(fail)].in_off) - BLOCK_SIZE_BYTES;
+				rs.checksum_first = info.block_checksum != 0;
+				g_last_path |= LZ4ADA_PATH_EXACT |
+				               (linked ? LZ4ADA_PATH_LINKED : LZ4ADA_PATH_INDEPENDENT);
+				phase("state");
+				try {
+					exact_frame(f, len, out, consumed, &rs);
+				} catch (...) {
+					phase("resume");
+					throw;
+				}
+				phase("resume");
+				return;
 			}
 			if (r == BULK_OK && (!info.has_content_size || total == info.content_size) &&
 			    (!h || (total == 0 ? 0x02cc5d05u : hs.hash) == info.content_checksum_declared)) {
@@ -1914,7 +2082,7 @@ int lz4ada_decode_stream(const uint8_t* input, int64_t len, uint8_t* out, int64_
 // The same into a buffer the library allocates and grows (no bound needed
 // up front); release it with lz4ada_buffer_free.  On failure *out is NULL.
 static int decode_alloc(const uint8_t* input, int64_t len, bool stream, uint8_t** out,
-                        int64_t* out_len, int64_t* consumed)
+                        int64_t* out_len, int64_t* consumed, bool keep_partial = false)
 {
 	*out = nullptr;
 	*out_len = 0;
@@ -1938,6 +2106,11 @@ static int decode_alloc(const uint8_t* input, int64_t len, bool stream, uint8_t*
 			*consumed = pos;
 	});
 	if (st != LZ4ADA_OK) {
+		if (keep_partial) {  // what the reference had output before it raised
+			*out = s.p ? s.p : static_cast<uint8_t*>(malloc(1));
+			*out_len = s.len;
+			return st;
+		}
 		free(s.p);
 		return st;
 	}
@@ -1955,6 +2128,12 @@ int lz4ada_decode_frame_alloc(const uint8_t* frame, int64_t len, uint8_t** out, 
 int lz4ada_decode_stream_alloc(const uint8_t* input, int64_t len, uint8_t** out, int64_t* out_len)
 {
 	return decode_alloc(input, len, true, out, out_len, nullptr);
+}
+
+int lz4ada_decode_frame_partial(const uint8_t* frame, int64_t len, uint8_t** out, int64_t* out_len,
+                                int64_t* frame_consumed)
+{
+	return decode_alloc(frame, len, false, out, out_len, frame_consumed, true);
 }
 
 void lz4ada_buffer_free(uint8_t* p) { free(p); }
@@ -1975,8 +2154,10 @@ int lz4ada_decode_linked_device(const void* d_frame, uint64_t frame_len,
 		};
 		ls.done = [&](const uint8_t*, int64_t n) { pos += n; };
 		uint64_t total = 0;
+		std::vector<uint32_t> lens;
+		int64_t fail = -1;
 		if (bulk_linked(static_cast<const uint8_t*>(d_frame), frame_len, block_max, v, ls, total,
-		                s) != BULK_OK)
+		                lens, fail, s) != BULK_OK)
 			raise(LZ4ADA_EXACT_PATH,
 			      "the frame needs the reference-exact path (lz4ada_decode_frame): a block "
 			      "error or checksum mismatch, quirk D1, or too little output room");

@@ -330,18 +330,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 		lo = uni(__builtin_amdgcn_alignbyte(w1, w0, sh));
 		hi = uni(__builtin_amdgcn_alignbyte(w2, w1, sh));
 	};
-	// the same into VGPRs (the fast parse path below stays on the VALU)
-	auto lds8v = [&](int32_t pos, uint32_t& lo, uint32_t& hi) {
-		const uint32_t a = uint32_t(pos + mis);
-		const uint32_t r0 = a & ~3u;
-		const uint32_t* w = reinterpret_cast<const uint32_t*>(S.ring);
-		const uint32_t w0 = w[(r0 & (RING - 1)) >> 2], w1 = w[((r0 + 4) & (RING - 1)) >> 2],
-		               w2 = w[((r0 + 8) & (RING - 1)) >> 2];
-		const uint32_t sh = a & 3u;
-		lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-		hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-		asm volatile("" : "+v"(lo), "+v"(hi));
-	};
 	auto rd8 = [&](int32_t pos, uint32_t& lo, uint32_t& hi) {
 		pos = int32_t(uni(uint32_t(pos)));
 		if (pos + mis + 8 > shi)

@@ -200,6 +200,7 @@ _sig = {
     "lz4ada_decode_stream": ([_vp, _i64, _vp, _i64, _pi64], ctypes.c_int),
     "lz4ada_decode_frame_alloc": ([_vp, _i64, _P(_vp), _pi64, _pi64], ctypes.c_int),
     "lz4ada_decode_stream_alloc": ([_vp, _i64, _P(_vp), _pi64], ctypes.c_int),
+    "lz4ada_decode_frame_partial": ([_vp, _i64, _P(_vp), _pi64, _pi64], ctypes.c_int),
     "lz4ada_buffer_free": ([_vp], None),
     "lz4ada_last_path": ([], ctypes.c_int),
     "lz4ada_release_device_cache": ([], None),
@@ -385,6 +386,19 @@ def decode_frame(data, offset: int = 0):
                                           ctypes.byref(olen), ctypes.byref(cons)),
            _thread_error())
     return _take(p, olen.value), cons.value
+
+
+def decode_frame_partial(data, offset: int = 0):
+    """One frame -> (decoded bytes, bytes consumed, exception or None).  On
+    an error the bytes are what the reference had output before raising
+    (every block before the failing one), as its CLI writes them."""
+    n = len(data) - offset
+    p, olen, cons = _vp(), _i64(), _i64()
+    st = _lib.lz4ada_decode_frame_partial(_addr(data, offset), n, ctypes.byref(p),
+                                          ctypes.byref(olen), ctypes.byref(cons))
+    out = _take(p, olen.value) if p.value else b""
+    exc = _ERRORS.get(st, LZ4AdaError)(_thread_error()) if st else None
+    return out, cons.value, exc
 
 
 def decode_stream(data) -> bytes:

@@ -286,6 +286,17 @@ int lz4ada_decode_stream_alloc(const uint8_t *input, int64_t len, uint8_t **out,
                                int64_t *out_len);
 void lz4ada_buffer_free(uint8_t *p);
 
+/* lz4ada_decode_frame_alloc, except that on failure *out / *out_len hold
+ * what the reference would have output before raising: every block before
+ * the failing one, each returned by its own Update call (lz4ada.adb:383-418,
+ * 661-714; tool_unlz4ada/unlz4ada.adb:41 writes each at once).  The exact
+ * path resumes at (or just before) the failing block with the stream state
+ * replayed from the decoded lengths, so the error comes in about the time
+ * the bulk path needs, not after a redo of the frame.  Free *out with
+ * lz4ada_buffer_free() in both cases. */
+int lz4ada_decode_frame_partial(const uint8_t *frame, int64_t len, uint8_t **out,
+                                int64_t *out_len, int64_t *frame_consumed);
+
 /* The linked-frame bulk path over a device-resident frame (BASELINE
  * configs[4]): every block at once against a synthetic history, resolved
  * on the GPU, into contiguous device output d_out

@@ -127,6 +127,12 @@ def d1_risk(blocks):
     return False
 
 
+def want_path(blocks):
+    """The linked bulk path takes the frame; at a D1 block the exact path
+    resumes and finishes it."""
+    return lz4ada.PATH_LINKED | (lz4ada.PATH_EXACT if d1_risk(blocks) else 0)
+
+
 # ------------------------------------------------------------ linked frames
 
 @pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "chain"])
@@ -146,8 +152,7 @@ def test_linked_frame_bulk(kind, bmax):
         with pytest.raises(lz4ada.LZ4AdaError) as ei:
             lz4ada.decode_frame(frame)
         assert str(ei.value) == O.exception_information(st, msg)
-    want = lz4ada.PATH_EXACT if d1_risk(blocks) else lz4ada.PATH_LINKED
-    assert lz4ada.last_path() == want
+    assert lz4ada.last_path() == want_path(blocks)
 
 
 def test_linked_frame_mixed_block_sizes():
@@ -160,7 +165,7 @@ def test_linked_frame_mixed_block_sizes():
     assert st == O.OK and ref == raw, msg
     out, _ = lz4ada.decode_frame(frame)
     assert out == raw
-    assert lz4ada.last_path() == (lz4ada.PATH_EXACT if d1_risk(blocks) else lz4ada.PATH_LINKED)
+    assert lz4ada.last_path() == want_path(blocks)
 
 
 @pytest.mark.parametrize("batch", [None, 300 * KiB, 1])
@@ -183,7 +188,7 @@ def test_linked_small_batches_64k(env):
     env("LZ4ADA_LINKED_BATCH_BYTES", str(200 * KiB))
     frame, raw, blocks = linked_frame(lz4ada.GEN_MIXED, [65536] * 9 + [4000], 64 * KiB, seed=3)
     same_as_oracle(frame)
-    assert lz4ada.last_path() == (lz4ada.PATH_EXACT if d1_risk(blocks) else lz4ada.PATH_LINKED)
+    assert lz4ada.last_path() == want_path(blocks)
 
 
 def d1_frame(content_cksum):
@@ -208,7 +213,8 @@ def test_d1_goes_exact_and_matches_reference():
     assert ref != spec  # the reference really diverges here
     out, _ = lz4ada.decode_frame(frame)
     assert out == ref
-    assert lz4ada.last_path() == lz4ada.PATH_EXACT
+    # block 0 through the linked bulk path, the exact path from block 1 on
+    assert lz4ada.last_path() == lz4ada.PATH_LINKED | lz4ada.PATH_EXACT
 
 
 def test_d1_with_content_checksum_raises_like_reference():
