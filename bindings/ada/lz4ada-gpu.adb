@@ -52,4 +52,18 @@ package body LZ4Ada.GPU is
 		return C_Decoded_Bound(Input'Address, Input'Length);
 	end Decoded_Bound;
 
+	procedure Decode_Frame_Multi(Frame:          in     Octets;
+				N_GPUs:         in     Positive;
+				Output:         in out Octets;
+				Output_Length:  out    Interfaces.Integer_64;
+				Frame_Consumed: out    Interfaces.Integer_64) is
+		L, C: aliased Interfaces.Integer_64;
+	begin
+		Check(C_Decode_Frame_Multi(Frame'Address, Frame'Length,
+			Interfaces.Integer_32(N_GPUs), System.Null_Address,
+			Output'Address, Output'Length, L'Access, C'Access));
+		Output_Length  := L;
+		Frame_Consumed := C;
+	end Decode_Frame_Multi;
+
 end LZ4Ada.GPU;

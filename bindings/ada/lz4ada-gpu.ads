@@ -22,6 +22,15 @@ package LZ4Ada.GPU is
 	-- lz4ada_decoded_bound: output capacity needed by Decode_Stream.
 	function Decoded_Bound(Input: in Octets) return Interfaces.Integer_64;
 
+	-- lz4ada_decode_frame_multi: Decode_Frame over GPUs 0 .. N_GPUs-1 of
+	-- this process (one host thread per device, RCCL for the verdict);
+	-- frames that do not shard decode on GPU 0.  Same exceptions.
+	procedure Decode_Frame_Multi(Frame:          in     Octets;
+				N_GPUs:         in     Positive;
+				Output:         in out Octets;
+				Output_Length:  out    Interfaces.Integer_64;
+				Frame_Consumed: out    Interfaces.Integer_64);
+
 private
 
 	function C_Decode_Frame(Frame: System.Address; Len: Interfaces.Integer_64;
@@ -39,5 +48,12 @@ private
 	function C_Decoded_Bound(Input: System.Address; Len: Interfaces.Integer_64)
 			return Interfaces.Integer_64;
 	pragma Import(C, C_Decoded_Bound, "lz4ada_decoded_bound");
+
+	function C_Decode_Frame_Multi(Frame: System.Address; Len: Interfaces.Integer_64;
+			N_GPUs: Interfaces.Integer_32; Devices: System.Address;
+			Out_Buf: System.Address; Out_Cap: Interfaces.Integer_64;
+			Out_Len, Consumed: access Interfaces.Integer_64)
+			return Interfaces.Integer_32;
+	pragma Import(C, C_Decode_Frame_Multi, "lz4ada_decode_frame_multi");
 
 end LZ4Ada.GPU;

@@ -1819,6 +1819,10 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 // (LZ4ADA_PATH_* bits; tests and diagnostics).
 static thread_local int g_last_path = 0;
 
+// for lz4ada_multi.cpp (lz4ada_internal.h)
+void set_thread_error(const std::string& msg) { g_thread_error = msg; }
+void set_last_path(int bits) { g_last_path = bits; }
+
 // The stream state before block `fail`, the first one the bulk path could
 // not take (its predecessors are committed): Output_Pos and
 // Output_Pos_History as lz4ada.adb:678-690 and 785-787 leave them.

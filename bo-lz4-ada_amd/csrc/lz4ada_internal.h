@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "lz4ada_hip.h"
 
 namespace lz4ada {
@@ -172,6 +174,11 @@ hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail
                             uint8_t* d_tail_new, hipStream_t stream);
 
 // Gather variable-length slots into a contiguous buffer (short blocks).
+// host side (lz4ada_host.cpp): the calling thread's message for
+// lz4ada_thread_last_error() and its lz4ada_last_path() bits
+void set_thread_error(const std::string& msg);
+void set_last_path(int bits);
+
 hipError_t launch_compact(const uint8_t* d_src, const lz4ada_block_desc* d_desc,
                           const uint64_t* d_dst_off, const lz4ada_block_status* d_status,
                           uint32_t nblocks, uint8_t* d_dst, hipStream_t stream);

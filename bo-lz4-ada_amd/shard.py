@@ -211,7 +211,10 @@ def decode_frame_sharded(frame: bytes, rank: int, world: int, device, group=None
     output stays resident on the rank's GPU (slots of block_max bytes).
     Raises the reference exception (via the exact path) if any rank found a
     bad block or the frame-level checks fail; linked frames raise ValueError
-    (they do not shard).  coll_device: device of the collectives' tensors
+    (they do not shard).  A frame with B.Indep set whose blocks read earlier
+    blocks decodes, as the reference decodes it, through the
+    one-GPU linked path: rank 0 returns it whole as one run ((0, nblocks),
+    [length]), the other ranks an empty range.  coll_device: device of the collectives' tensors
     (default `device`; "cpu" for a gloo group)."""
     coll = coll_device if coll_device is not None else device
     info, descs = lz4ada.frame_index(frame)
@@ -246,10 +249,14 @@ def decode_frame_sharded(frame: bytes, rank: int, world: int, device, group=None
                              lambda: _product_hasher(d_out, runs, stream.cuda_stream),
                              rank, world, group, coll)
     if not ok:
-        lz4ada.decode_frame(frame)  # raises the reference exception
+        out, _ = lz4ada.decode_frame(frame)  # raises the reference exception
         # the single-GPU path accepted it: a block reaches before its own
         # start (B.Indep set but ignored by the reference) ->
-        # linked data, decoded by the linked path
-        raise ValueError("frame has cross-block references (D2); decode it on one GPU "
-                         "with lz4ada.decode_frame")
+        # linked data, decoded by the linked path.  It does not shard: rank 0
+        # holds the whole output as one run, the other ranks nothing.
+        n = info.nblocks
+        if rank != 0:
+            return torch.empty(1, dtype=torch.uint8, device=device), (n, n), []
+        d = torch.frombuffer(bytearray(out or b"\0"), dtype=torch.uint8).to(device)
+        return d, (0, n), [len(out)]
     return d_out, (lo, hi), out_lens

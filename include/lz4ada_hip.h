@@ -315,6 +315,7 @@ int lz4ada_decode_linked_device(const void *d_frame, uint64_t frame_len,
 #define LZ4ADA_PATH_INDEPENDENT 1
 #define LZ4ADA_PATH_LINKED 2
 #define LZ4ADA_PATH_EXACT 4
+#define LZ4ADA_PATH_MULTI 8 /* lz4ada_decode_frame_multi* took the call */
 int lz4ada_last_path(void);
 
 /* The bulk path keeps its large device scratch (output slots, linked-frame
@@ -324,6 +325,39 @@ void lz4ada_release_device_cache(void);
 /* Upper bound of the decoded size of a stream (sum of block maxima); -1 if
  * some frame does not index (then use the _alloc calls). */
 int64_t lz4ada_decoded_bound(const uint8_t *input, int64_t len);
+
+/* ------------------------------------------------- multi-GPU bulk decode */
+/*
+ * One frame over n_gpus devices from ONE process (no
+ * reference twin -- it replaces the caller's whole Update loop
+ * (lz4ada.ads:281-287, tool_unlz4ada/unlz4ada.adb:84-103) for a frame, like
+ * lz4ada_decode_frame, and spreads it over GPUs).  An independent-block
+ * modern frame is split into contiguous block ranges balanced by compressed
+ * bytes (lz4ada_plan_shards); one host worker thread per device copies its
+ * range in and decodes it; RCCL (ncclCommInitAll over the devices) carries
+ * one all-reduce of the block verdict and the per-device output sizes, and
+ * for the _gather variant the bytes to the first device.  The content
+ * checksum is one XXH32 chain in frame order.  Linked, legacy and skippable
+ * frames, and any frame the bulk path would not take (block error, checksum
+ * mismatch, cross-block references, failed frame checks), are decoded by
+ * lz4ada_decode_frame on the first device, which gives the reference's
+ * output or exception.  devices: n_gpus HIP ordinals, or NULL for
+ * 0 .. n_gpus-1.  Calls are serialised (the communicators are shared).
+ */
+int lz4ada_decode_frame_multi(const uint8_t *frame, int64_t len, int n_gpus, const int *devices,
+                              uint8_t *out, int64_t out_cap, int64_t *out_len,
+                              int64_t *frame_consumed);
+/* The same with the output gathered into d_out on the first device
+ * (out_cap bytes, device memory) instead of host memory. */
+int lz4ada_decode_frame_multi_gather(const uint8_t *frame, int64_t len, int n_gpus,
+                                     const int *devices, void *d_out, int64_t out_cap,
+                                     int64_t *out_len, int64_t *frame_consumed);
+/* The block split of the above (and of bo-lz4-ada_amd/shard.py): rank r
+ * decodes blocks [bounds[r], bounds[r+1]) (bounds has n_gpus + 1 entries);
+ * the blocks whose compressed-prefix midpoint falls in
+ * [r, r+1) * total / n_gpus.  Host-only. */
+int lz4ada_plan_shards(const lz4ada_block_desc *descs, int64_t nblocks, int n_gpus,
+                       int64_t *bounds);
 
 /* ------------------------------------------------------------------ misc */
 

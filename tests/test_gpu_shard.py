@@ -105,9 +105,12 @@ def test_sharded_frame_checks(what, world):
         assert pos == len(raw)
     elif what == "d2":
         # B.Indep set, blocks read earlier blocks: the reference decodes it
-        # (linked), so the shards refuse and point at the one-GPU path
+        # (linked); it does not shard, rank 0 returns it whole
         assert st == O.OK and ref == raw, msg
-        assert [r[1] for r in res] == ["value"] * world
+        assert [r[1] for r in res] == ["ok"] * world
+        n, h = res[0][2]
+        assert n == len(raw) and h == lz4frame.xxhash.xxh32(raw).intdigest()
+        assert all(r[2][0] == 0 for r in res[1:])
     else:
         assert st != O.OK
         want = O.exception_information(st, msg)
