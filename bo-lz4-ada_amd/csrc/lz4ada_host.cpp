@@ -686,13 +686,11 @@ struct lz4ada_decompressor {
 	}
 
 	// A lone block is latency-bound: the 512-lane workgroup decoder (blocks
-	// it declines are redone by the one-wave decoder) decodes a 4 MiB block
+	// it declines are redone by the two-wave decoder) decodes a 4 MiB block
 	// ~1.6x sooner than the two-wave decoder (tools/facade_time.py).
 	static int facade_variant()
 	{
 		const char* e = getenv("LZ4ADA_FACADE_DECODER");
-		if (e && !strcmp(e, "wave"))
-			return DEC_WAVE;
 		if (e && !strcmp(e, "pc"))
 			return DEC_PC;
 		return DEC_WG;

@@ -68,7 +68,7 @@ struct SerialState {
 // All launch on `stream` and never synchronise.
 
 // Bulk independent-block decoders (LZ4ADA_DECODE_* in lz4ada_hip.h).
-enum DecVariant : int { DEC_PC = 0, DEC_WAVE = 1, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4,
+enum DecVariant : int { DEC_PC = 0, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4,
                         DEC_IDX_LINKED = 5, DEC_IDX_SPARSE = 6 };
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
@@ -76,8 +76,9 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
                                  uint8_t* d_out, lz4ada_block_status* d_status, int variant,
                                  hipStream_t stream);
 
-// The default decoder: k_decode_pc (producer + consumer wave per block);
-// LZ4ADA_DECODER=wave / wg select the others.
+// The default decoder: the index-driven decoder, then the literal-heavy and
+// two-wave decoders for the blocks it declines; LZ4ADA_DECODER=pc / wg
+// select the others.
 hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                 uint8_t* d_out, lz4ada_block_status* d_status,

@@ -6,20 +6,14 @@
 //   Output_With_History (overlap-safe match copy)    :845-904
 //
 // (XXH32: lz4ada_xxh32.hip.)  Design (DESIGN.md has the long form):
-//  * k_decode_blocks -- one 64-lane wavefront per independent block.  The
-//    compressed stream is staged through a 1 KiB LDS window with 16 B/lane
-//    loads.  Token boundaries are found speculatively: every lane parses a
-//    token at 4 of the next 256 byte positions, the chain from the known
-//    start is resolved by pointer doubling (6 LDS jump tables) and lane j
-//    picks up the j-th token -- up to 64 sequences per step instead of one.
-//    Output offsets come from a wave prefix scan; literals are copied into
-//    a 4 KiB LDS batch buffer, matches are copied lane-parallel in
-//    dependency rounds (a lane runs once every earlier match it reads from
-//    is final), then the batch is flushed to HBM.  Overlapping matches use
-//    src = start - off + (k mod off), so a lane never waits on its own
-//    output.  Long or unusual tokens (multi-byte length extensions, runs
-//    over 256 B, anything malformed) go through a wave-cooperative
-//    one-token path that also produces the precise error.
+//  * k_decode_pc -- two waves per block (producer parses windows of
+//    sequences speculatively, consumer copies them); the bulk path's
+//    decoder for the blocks the index-driven decoder (lz4ada_idx.hip) and
+//    the literal-heavy decoder (lz4ada_sparse.hip) decline, and the lone
+//    facade block's fallback after the workgroup decoder (lz4ada_wg.hip).
+//    Long or unusual tokens (multi-byte length extensions, anything
+//    malformed) go through a wave-cooperative one-token path that also
+//    produces the precise error.
 //  * k_serial_block -- reference-exact single-lane emulation of one block
 //    on a device mirror of the caller's Buffer (Output_Pos wrap, history,
 //    8-byte wild-copy overshoot and its D1 side effect).  Used by the
@@ -55,7 +49,7 @@ static_assert(SPAN + BIG + 64 + STAGE_AHEAD + 1024 + 16 <= INB, "input ring too 
 enum TokKind : int { TK_NORMAL = 0, TK_LAST = 1, TK_COMPLEX = 2, TK_ERR = 3 };
 
 // Diagnostic build only (make stamps -> liblz4ada_hip_stamps.so): per-phase
-// s_memtime sums of k_decode_blocks, read back by tools/stamps.py.  The
+// s_memtime sums of the decoders' phases, read back by tools/stamps.py.  The
 // product library is built without LZ4ADA_STAMPS and executes no stamp.
 enum StampPhase { SP_STAGE, SP_CAND, SP_DOUBLE, SP_SELECT, SP_LIT, SP_MATCH, SP_FLUSH, SP_ONE,
 	          SP_WAIT, SP_DEP, SP_BATCHES, SP_WINDOWS, SP_TOKENS, SP_ROUNDS, SP_N };
@@ -86,17 +80,6 @@ __device__ unsigned long long g_stamps[SP_N];
 #define STAMP_ARGS
 #define STAMP_FLUSH()
 #endif
-
-__device__ __forceinline__ int64_t wave_min_i64(int64_t v)
-{
-#pragma unroll
-	for (int m = 32; m >= 1; m >>= 1) {
-		int64_t o = __shfl_xor(v, m);
-		v = o < v ? o : v;
-	}
-	return v;
-}
-
 
 // Sum of a length extension (Process_Variable_Length, lz4ada.adb:724-735)
 // starting at block-relative p, 64 bytes per step.  Returns false when the
@@ -449,17 +432,6 @@ __device__ __forceinline__ int32_t owner_of(int32_t ts_reg, int32_t nb, int32_t 
 	return lo;
 }
 
-struct alignas(16) DecLds {
-	uint16_t J[6][WIN];         // J[r][k]: window position 2^r tokens after k (>= WIN: out)
-	uint8_t inb[INB + MIRROR];  // block-relative x -> inb[(x + mis) & INB_MASK]
-	uint8_t outb[OUTB + 32];    // batch output
-	int32_t r_tstart[MAXTOK];   // batch tokens: output start (batch-relative)
-	int32_t r_L[MAXTOK];
-	int32_t r_lit[MAXTOK];
-	int32_t r_off[MAXTOK];
-	int32_t r_ml[MAXTOK];
-};
-
 // Cross-lane hand-off through LDS inside one wavefront: LDS executes a
 // wave's operations in order, so only the compiler must not reorder.
 
@@ -509,382 +481,6 @@ __device__ __forceinline__ void stage_to(LdsT& L, cg8* in, uintptr_t lim_addr, i
 }
 
 // Exact-length store of n (0..16) bytes of v to LDS.
-
-__global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t* __restrict__ frame,
-                                                       uint64_t frame_len,
-                                                       const lz4ada_block_desc* __restrict__ desc,
-                                                       uint32_t nblocks, uint8_t* __restrict__ out,
-                                                       lz4ada_block_status* __restrict__ status,
-                                                       int retry_only)
-{
-	__shared__ DecLds L;
-
-	const uint32_t b = blockIdx.x;
-	if (b >= nblocks)
-		return;
-	if (retry_only && status[b].code != DS_RETRY && status[b].code != DS_SPARSE)
-		return;
-	const int lane = int(lane_id());
-	const lz4ada_block_desc d = desc[b];
-	cg8* __restrict__ in = gptr(frame) + d.in_off;
-	g8* __restrict__ ob = gptr(out) + d.out_off;
-	const int32_t n = int32_t(d.in_len);
-	const int32_t cap = int32_t(d.out_cap);
-
-	lz4ada_block_status st;
-	st.code = DS_OK;
-	st.aux = 0;
-	st.detail = 0;
-	st.err_out_pos = 0;
-	st.out_len = 0;
-
-	if (d.flags & LZ4ADA_BLOCK_STORED) {
-		if (n > cap) {
-			st.code = DS_OUT_OVERFLOW;
-		} else {
-			wave_copy(ob, in, n);
-			st.out_len = uint32_t(n);
-		}
-		if (lane == 0) {
-			status[b].code = st.code;
-			status[b].aux = 0;
-			status[b].detail = 0;
-			status[b].err_out_pos = 0;
-			status[b].out_len = st.out_len;
-		}
-		return;
-	}
-
-	const uintptr_t lim_addr = reinterpret_cast<uintptr_t>(frame) + frame_len;
-	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
-	int32_t s = 0;       // block-relative compressed position of the chain
-	int32_t o = 0;       // block-relative output position (flushed)
-	int32_t hi = -mis;   // staged compressed bytes end (block-relative)
-	u32x4 pf0 = load_chunk(in, lim_addr, hi);
-	u32x4 pf1 = load_chunk(in, lim_addr, hi + 1024);
-	int32_t nb = 0;      // tokens in the current batch
-	int32_t blen = 0;    // batch output bytes
-	int32_t bcomp0 = 0;  // compressed position of the batch's first token
-	bool ok = true;
-	bool done = (n == 0);
-	STAMP_DECL;
-
-	for (int32_t iter = 0; !done; ++iter) {
-		if (iter > 4 * n + 64) {  // every iteration makes progress; never spin
-			st.code = DS_INTERNAL;
-			ok = false;
-			break;
-		}
-		// ------------------------------------------------ window parse at s
-		bool stop = false, end_block = false, force_flush = false;
-		{
-			// keep the ring ahead of the chain: a window needs s + 64 + LOOK,
-			// a serial long-literal token up to s + BIG + 16
-			stage_to(L, in, lim_addr, mis, hi, pf0, pf1, nb ? bcomp0 : s, s + STAGE_AHEAD);
-			STAMP(SP_STAGE);
-			STAMP_COUNT(SP_WINDOWS, 1);
-		}
-		// a literal run with a multi-byte extension will not fit a window:
-		// parse it serially from the ring instead of speculatively
-		const uint32_t peek = uint32_t(uni(int32_t(lds_u16(L.inb + ((s + mis) & INB_MASK)))));
-		if ((peek & 0xf0u) == 0xf0u && (peek >> 8) == 255u && s + 1 < n) {
-			Cand t = {};
-			bool okp = parse_serial(L.inb, mis, s, n, hi, t);
-			const int32_t klen = t.L + t.ml;
-			const int32_t d0 = o + blen + t.L;
-			okp = okp && nb < MAXTOK && klen <= BIG && blen + klen <= OUTB &&
-			      o + blen + klen <= cap && (t.kind != TK_NORMAL || d0 - t.off >= 0) &&
-			      (t.off >= 16 || t.ml <= 64);
-#ifdef LZ4ADA_TRACE_POS
-			if (b == 0 && lane == 0 && o + blen <= LZ4ADA_TRACE_POS + 4096 && LZ4ADA_TRACE_POS < o + blen + 8192)
-				printf("[trace] serial s=%d okp=%d L=%d lit=%d off=%d ml=%d next=%d kind=%d nb=%d blen=%d o=%d hi=%d\n",
-				       s, int(okp), t.L, t.lit, t.off, t.ml, t.next, t.kind, nb, blen, o, hi);
-#endif
-			if (okp) {
-				if (lane == 0) {
-					L.r_tstart[nb] = blen;
-					L.r_L[nb] = t.L;
-					L.r_lit[nb] = t.lit;
-					L.r_off[nb] = t.off;
-					L.r_ml[nb] = t.ml;
-				}
-				if (nb == 0)
-					bcomp0 = s;
-				++nb;
-				blen += klen;
-				STAMP_COUNT(SP_TOKENS, 1);
-				if (t.kind == TK_LAST || t.next >= n) {
-					end_block = true;
-					s = t.next;
-				} else {
-					s = t.next;
-				}
-			} else if (nb == 0) {
-				stop = true;
-			} else {
-				force_flush = true;
-			}
-		} else {
-			// candidates at s + [0, WIN): next-token pointers
-#pragma unroll
-			for (int q = 0; q < WIN / 64; ++q) {
-				const int k = 64 * q + lane;
-				const Cand t = parse_cand(L.inb, mis, s + k, n);
-				const int32_t rel = t.next - s;
-				L.J[0][k] = uint16_t((t.kind == TK_NORMAL && rel < WIN) ? rel : 0xffff);
-			}
-			wave_lds_fence();
-			STAMP(SP_CAND);
-			// pointer doubling: J[r+1][k] = J[r][J[r][k]]
-#pragma unroll
-			for (int r = 0; r < 5; ++r) {
-				uint32_t a[WIN / 64];
-#pragma unroll
-				for (int q = 0; q < WIN / 64; ++q)
-					a[q] = L.J[r][64 * q + lane];
-#pragma unroll
-				for (int q = 0; q < WIN / 64; ++q)
-					a[q] = a[q] < WIN ? L.J[r][a[q]] : 0xffffu;
-#pragma unroll
-				for (int q = 0; q < WIN / 64; ++q)
-					L.J[r + 1][64 * q + lane] = uint16_t(a[q]);
-				wave_lds_fence();
-			}
-			STAMP(SP_DOUBLE);
-			// lane j: window position of the j-th token of the chain from s
-			uint32_t cj = 0;
-#pragma unroll
-			for (int r = 0; r < 6; ++r) {
-				const uint32_t g = cj < WIN ? L.J[r][cj] : 0xffffu;
-				if ((lane >> r) & 1)
-					cj = g;
-			}
-			const bool inwin = cj < WIN;
-			const Cand tk = parse_cand(L.inb, mis, s + (inwin ? int32_t(cj) : 0), n);
-			const int32_t kL = tk.L, klit = tk.lit, koff = tk.off, kml = tk.ml;
-			const int32_t knext = tk.next, kkind = tk.kind;
-			const bool good = inwin && (kkind == TK_NORMAL || kkind == TK_LAST);
-			const int32_t klen = kL + kml;
-			const int32_t incl = wave_incl_scan(good ? klen : 0);
-			const int32_t tstart = blen + incl - klen;
-			const int32_t d0 = o + tstart + kL;  // block-relative match start
-			const bool fits = good && lane < MAXTOK - nb && klen <= BIG && blen + incl <= OUTB &&
-			                  o + blen + incl <= cap && (kkind != TK_NORMAL || d0 - koff >= 0) &&
-			                  (koff >= 16 || kml <= 64);
-			const uint64_t badm = __ballot(!fits);
-			const int cnt = badm ? (__ffsll((long long)badm) - 1) : 64;
-			const int32_t cnext = cnt > 0 ? __shfl(knext, cnt - 1) : s;
-			const int32_t ckind_last = cnt > 0 ? __shfl(kkind, cnt - 1) : TK_NORMAL;
-			if (lane < cnt) {
-				L.r_tstart[nb + lane] = tstart;
-				L.r_L[nb + lane] = kL;
-				L.r_lit[nb + lane] = klit;
-				L.r_off[nb + lane] = koff;
-				L.r_ml[nb + lane] = kml;
-			}
-			STAMP_COUNT(SP_TOKENS, cnt);
-#ifdef LZ4ADA_TRACE_POS
-			if (b == 0 && lane < cnt && o + tstart <= LZ4ADA_TRACE_POS + 4096 && LZ4ADA_TRACE_POS < o + tstart + 8192)
-				printf("[trace] window s=%d lane=%d cj=%u L=%d lit=%d off=%d ml=%d next=%d tstart=%d nb=%d o=%d\n",
-				       s, lane, cj, kL, klit, koff, kml, knext, tstart, nb, o);
-#endif
-			const bool was_empty = (nb == 0);
-			if (was_empty && cnt > 0)
-				bcomp0 = s;
-			nb += cnt;
-			blen += cnt > 0 ? __shfl(incl, cnt - 1) : 0;
-			if (cnt > 0 && ckind_last == TK_LAST) {
-				end_block = true;
-				s = n;
-			} else if (cnt > 0 && cnext >= n) {
-				end_block = true;  // block ends right after a match (lz4ada.adb:780)
-				s = cnext;
-			} else if (cnt > 0) {
-				s = cnext;
-			} else if (was_empty) {
-				stop = true;  // the token at s needs the one-token path
-			} else {
-				force_flush = true;  // batch full: flush, then retry at s
-			}
-		}
-		wave_lds_fence();
-		STAMP(SP_SELECT);
-		const bool flush = end_block || stop || force_flush || nb > MAXTOK - WTOK / 2 ||
-		                   blen > OUTB - BIG || (s - bcomp0) >= SPAN;
-		if (flush && nb > 0) {
-			// -------------------------------------------- batch copy
-			const bool tl = lane < nb;
-			const int32_t ts = tl ? L.r_tstart[lane] : 0;
-			const int32_t tL = tl ? L.r_L[lane] : 0;
-			const int32_t tlit = tl ? L.r_lit[lane] : 0;
-			const int32_t toff = tl ? L.r_off[lane] : 1;
-			const int32_t tml = tl ? L.r_ml[lane] : 0;
-			// first 32 bytes of every pre-batch match source: loads issued now,
-			// consumed in the match rounds, so their latency hides under the
-			// literal copy
-			const int32_t d0 = ts + tL;               // batch-relative
-			const int32_t q0 = o + d0 - toff;         // block-relative source
-			u32x4 pv0 = {0, 0, 0, 0}, pv1 = {0, 0, 0, 0};
-			const bool pre0 = tl && tml > 0 && toff >= 16 && q0 + 16 <= o;
-			const bool pre1 = pre0 && tml > 16 && q0 + 32 <= o;
-#ifndef LZ4ADA_EXP_NOGLOBAL
-			if (pre0)
-				__builtin_memcpy(&pv0, (const uint8_t*)(ob + q0), 16);
-			if (pre1)
-				__builtin_memcpy(&pv1, (const uint8_t*)(ob + q0 + 16), 16);
-#endif
-			// literals: ring -> batch buffer, exact length.  Short runs: one
-			// lane per token; long runs: the whole wave, one token at a time.
-			constexpr int32_t LONG = 48;
-			if (tL <= LONG) {
-				for (int32_t i = 0; i < tL; i += 16) {
-					u32x4 v;
-					__builtin_memcpy(&v, &L.inb[(tlit + i + mis) & INB_MASK], 16);
-					lds_store_n(&L.outb[ts + i], v, tL - i);
-				}
-			}
-			for (uint64_t lm = __ballot(tl && tL > LONG); lm; lm &= lm - 1) {
-				const int k = __ffsll((long long)lm) - 1;
-				const int32_t Lk = __shfl(tL, k), litk = __shfl(tlit, k), tsk = __shfl(ts, k);
-				for (int32_t i = 16 * lane; i < Lk; i += 1024) {
-					u32x4 v;
-					__builtin_memcpy(&v, &L.inb[(litk + i + mis) & INB_MASK], 16);
-					lds_store_n(&L.outb[tsk + i], v, Lk - i);
-				}
-			}
-			wave_lds_fence();
-			STAMP(SP_LIT);
-			STAMP_COUNT(SP_BATCHES, 1);
-			// matches.  dep = earlier tokens whose match region overlaps this
-			// token's in-batch source range [a, b); a token copies in the
-			// first round in which none of them is pending.
-			const int32_t sb = (q0 + tml < o + d0 ? q0 + tml : o + d0) - o;
-			const int32_t sa = (q0 - o > 0) ? q0 - o : 0;
-			const bool inbatch = tl && tml > 0 && sb > 0;
-			uint64_t dep = 0;
-			if (__ballot(inbatch)) {
-				const int32_t ka = owner_of(ts, nb, inbatch ? sa : 0);
-				const int32_t kb = owner_of(ts, nb, inbatch ? sb - 1 : 0);
-				const int32_t d0_ka = __shfl(d0, ka), ml_ka = __shfl(tml, ka);
-				const int32_t d0_kb = __shfl(d0, kb), ml_kb = __shfl(tml, kb);
-				if (inbatch) {
-					if (kb > ka + 1)
-						dep = ((1ull << kb) - 1) & ~((2ull << ka) - 1);
-					if (ml_ka > 0 && d0_ka < sb && d0_ka + ml_ka > sa)
-						dep |= 1ull << ka;
-					if (kb != ka && ml_kb > 0 && d0_kb < sb)
-						dep |= 1ull << kb;
-					dep &= (1ull << lane) - 1;  // own literals are final already
-				}
-			}
-			bool pend = tl && tml > 0;
-			for (int guard = 0; ; ++guard) {
-				const uint64_t pm = __ballot(pend);
-				if (!pm)
-					break;
-				const bool ready = pend && (!(pm & dep) || guard > MAXTOK);
-#ifdef LZ4ADA_TRACE_POS
-				if (ready && b == 0 && o + d0 <= LZ4ADA_TRACE_POS && LZ4ADA_TRACE_POS < o + d0 + tml)
-					printf("[trace] match lane=%d o=%d ts=%d tL=%d d0=%d off=%d ml=%d q0=%d nb=%d blen=%d guard=%d\n",
-					       lane, o, ts, tL, d0, toff, tml, q0, nb, blen, guard);
-#endif
-				if (ready) {
-					if (toff >= 16) {
-						// 16-byte chunks; a chunk's source ends before its
-						// destination starts, so own output is already there
-						for (int32_t i = 0; i < tml; i += 16) {
-							const int32_t sp = q0 + i;
-							const int32_t nn = tml - i < 16 ? tml - i : 16;
-							u32x4 v;
-							if (i == 0 && pre0) {
-								v = pv0;
-							} else if (i == 16 && pre1) {
-								v = pv1;
-							} else if (sp + 16 <= o) {
-#ifdef LZ4ADA_EXP_NOGLOBAL
-								v = pv0;
-#else
-								__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
-#endif
-							} else if (sp >= o) {
-								__builtin_memcpy(&v, &L.outb[sp - o], 16);
-							} else {
-								uint8_t t[16];
-								for (int k = 0; k < 16; ++k)
-									t[k] = (sp + k < o) ? ob[sp + k] : L.outb[sp + k - o];
-								__builtin_memcpy(&v, t, 16);
-							}
-							lds_store_n(&L.outb[d0 + i], v, nn);
-						}
-					} else {
-						// short offset: byte k repeats source byte (k mod off)
-						int32_t r = 0;
-						for (int32_t k = 0; k < tml; ++k) {
-							const int32_t sp = q0 + r;
-							L.outb[d0 + k] = (sp < o) ? ob[sp] : L.outb[sp - o];
-							if (++r == toff)
-								r = 0;
-						}
-					}
-				}
-				pend = pend && !ready;
-				wave_lds_fence();
-				STAMP_COUNT(SP_ROUNDS, 1);
-			}
-			STAMP(SP_MATCH);
-			// flush the batch to HBM
-			{
-				g8* dst = ob + o;
-				const int32_t head = int32_t((16 - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
-				const int32_t h = head < blen ? head : blen;
-				if (lane < h)
-					dst[lane] = L.outb[lane];
-				const int32_t nv = (blen - h) / 16;
-				for (int32_t i = lane; i < nv; i += 64) {
-					u32x4 v;
-					__builtin_memcpy(&v, &L.outb[h + 16 * i], 16);
-					*reinterpret_cast<GLOBAL u32x4*>(dst + h + 16 * i) = v;
-				}
-				for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)
-					dst[i] = L.outb[i];
-			}
-			__syncthreads();  // HBM writes visible to this wave's later loads
-#ifdef LZ4ADA_TRACE_POS
-			if (b == 0 && lane == 0 && o <= LZ4ADA_TRACE_POS + 4096 && LZ4ADA_TRACE_POS < o + blen + 4096)
-				printf("[trace] flush o=%d blen=%d nb=%d bcomp0=%d s=%d hi=%d\n", o, blen, nb, bcomp0, s, hi);
-#endif
-			STAMP(SP_FLUSH);
-			o += blen;
-			nb = 0;
-			blen = 0;
-		}
-		if (end_block) {
-			done = true;
-		} else if (stop) {
-			int64_t s64 = s, o64 = o;
-			bool d1_unused = false;
-			if (!one_token(in, n, ob, cap, s64, o64, st, 0, d1_unused)) {
-				ok = false;
-				done = true;
-			} else {
-				s = int32_t(s64);
-				o = int32_t(o64);
-				if (s >= n)
-					done = true;
-			}
-			STAMP(SP_ONE);
-		}
-	}
-	STAMP_FLUSH();
-
-	if (lane == 0) {
-		status[b].code = ok ? int32_t(DS_OK) : st.code;
-		status[b].aux = st.aux;
-		status[b].detail = st.detail;
-		status[b].err_out_pos = st.err_out_pos;
-		status[b].out_len = uint32_t(o);
-	}
-}
 
 // ------------------------------------------- producer/consumer decoder
 // k_decode_pc: the per-wave decoder split over two waves of one workgroup
@@ -1824,8 +1420,11 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 		if (err != hipSuccess)
 			return err;
 	}
-	hipLaunchKernelGGL(k_decode_blocks, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
-	                   d_desc, nblocks, d_out, d_status, variant == DEC_WG ? 1 : 0);
+	if (variant != DEC_WG)
+		return hipErrorInvalidValue;  // 1 was the round-1 one-wave decoder (retired)
+	// the blocks the workgroup decoder declined
+	hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
+	                   d_desc, nblocks, d_out, d_status, 1, 0);
 	return hipGetLastError();
 }
 
@@ -1855,16 +1454,14 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
 static int decoder_variant()
 {
 	// Default: the index-driven decoder (lz4ada_idx.hip), the two-wave
-	// decoder for the blocks it declines.  LZ4ADA_DECODER=pc / wave / wg
-	// select the two-wave, one-wave or experimental workgroup decoder.
+	// decoder for the blocks it declines.  LZ4ADA_DECODER=pc / wg select
+	// the two-wave or the workgroup decoder.
 	static const int variant = [] {
 		const char* e = getenv("LZ4ADA_DECODER");
 		if (e && e[0] == 'w' && e[1] == 'g')
 			return int(DEC_WG);
 		if (e && e[0] == 'p')
 			return int(DEC_PC);
-		if (e && e[0] == 'w')
-			return int(DEC_WAVE);
 		return int(DEC_IDX);
 	}();
 	return variant;

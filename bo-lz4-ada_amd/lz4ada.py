@@ -498,14 +498,14 @@ def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=
                                      stream), _thread_error())
 
 
-DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE, DECODE_IDX_LINKED = 0, 1, 2, 3, 4, 5
+DECODE_PC, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE, DECODE_IDX_LINKED = 0, 2, 3, 4, 5
 DECODE_IDX_SPARSE = 6
 
 
 def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,
                           stream=0):
     """One of the bulk decoders: DECODE_IDX (default: index-driven + two-wave
-    retry), DECODE_PC, DECODE_WAVE, DECODE_WG, DECODE_IDX_ALONE."""
+    retry), DECODE_PC, DECODE_WG, DECODE_IDX_ALONE."""
     _check(_lib.lz4ada_launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out,
                                              d_status, variant, stream), _thread_error())
 

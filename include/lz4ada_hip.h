@@ -225,11 +225,11 @@ int lz4ada_decode_blocks_device(const void *d_frame, uint64_t frame_len,
 int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
                          const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                          lz4ada_block_status *d_status, void *stream);
-/* Decoder variants of the bulk path: the default two-wave
- * producer/consumer decoder, the one-wave decoder, and the experimental
- * workgroup decoder followed by the one-wave decoder for declined blocks. */
+/* Decoder variants of the bulk path: the two-wave
+ * producer/consumer decoder, and the workgroup decoder followed by the
+ * two-wave decoder for declined blocks (1, the round-1 one-wave decoder, is
+ * retired: LZ4ADA_DEVICE_ERROR). */
 #define LZ4ADA_DECODE_PC 0
-#define LZ4ADA_DECODE_WAVE 1
 #define LZ4ADA_DECODE_WG 2
 /* Index-driven two-pass decoder (k_index + k_decode_idx, lz4ada_idx.hip),
  * then the two-wave decoder for the blocks it declines; _ALONE skips that
