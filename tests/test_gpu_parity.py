@@ -464,6 +464,27 @@ def test_idx_decoder_stored_and_small():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
+def oracle_blocks(frame, nblocks):
+    """The first frame's blocks as the oracle's Update returns them (one per
+    call; zero-length blocks included, from the size words)."""
+    import ctypes
+    info, descs = lz4ada.frame_index(frame)
+    ctx = O.Decompressor.init()
+    buf = ctypes.create_string_buffer(ctx.min_buffer_size)
+    blocks, pos = [], 0
+    while len(blocks) < nblocks and pos < len(frame):
+        st, c, f, l = ctx.update(frame[pos:pos + 4096], buf)
+        assert st == O.OK, ctx.last_error()
+        if l >= f:
+            blocks.append(buf.raw[f:l + 1])
+        pos += c
+        # a block that decodes to nothing returns no output: account for it
+        while len(blocks) < nblocks and descs[len(blocks)].in_len == 0 and \
+                not descs[len(blocks)].flags & lz4ada.BLOCK_STORED:
+            blocks.append(b"")
+    return blocks
+
+
 def test_idx_decoder_on_vectors(name, digests):
     """Reference vectors' blocks through the idx decoder (+ retry): every block
     byte-exact; linked blocks that reference earlier blocks are declined
@@ -474,11 +495,19 @@ def test_idx_decoder_on_vectors(name, digests):
     for i in range(info.nblocks):
         assert st[i].code in (0, lz4ada.DS_RETRY, lz4ada.DS_SPARSE), (i, st[i].code)
     descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX)
-    if info.independent or all(s.code == 0 for s in st[:info.nblocks]):
-        pieces = [out[i * info.block_max:i * info.block_max + st[i].out_len]
-                  for i in range(info.nblocks)]
-        if all(s.code == 0 for s in st[:info.nblocks]):
-            assert hashlib.sha256(b"".join(pieces)).hexdigest() == digests[name]["sha256"]
+    pieces = [out[i * info.block_max:i * info.block_max + st[i].out_len]
+              for i in range(info.nblocks)]
+    if all(s.code == 0 for s in st[:info.nblocks]):
+        assert hashlib.sha256(b"".join(pieces)).hexdigest() == digests[name]["sha256"]
+    # block by block against the oracle's Update outputs (one block per
+    # call, lz4ada.adb:383-418), for every block the bulk decoders took --
+    # also when others were declined
+    ref = oracle_blocks(frame, info.nblocks)
+    assert len(ref) == info.nblocks
+    took = [i for i in range(info.nblocks) if st[i].code == 0]
+    assert took or not info.nblocks, "no block was decoded"
+    for i in took:
+        assert pieces[i] == ref[i], i
 
 
 # ------------------------------------------- linked frames (BASELINE configs[4])
