@@ -462,8 +462,6 @@ def test_idx_decoder_stored_and_small():
     assert got == raw
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
 def oracle_blocks(frame, nblocks):
     """The first frame's blocks as the oracle's Update returns them (one per
     call; zero-length blocks included, from the size words)."""
@@ -485,6 +483,8 @@ def oracle_blocks(frame, nblocks):
     return blocks
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
 def test_idx_decoder_on_vectors(name, digests):
     """Reference vectors' blocks through the idx decoder (+ retry): every block
     byte-exact; linked blocks that reference earlier blocks are declined
