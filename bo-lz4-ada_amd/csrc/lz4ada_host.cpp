@@ -410,6 +410,7 @@ struct lz4ada_decompressor {
 	DevBuf<lz4ada_block_desc> d_desc;  // one-block fast path
 	DevBuf<lz4ada_block_status> d_bst;
 	DevBuf<uint8_t> d_scr;  // its output, until the block checksum has passed
+	DevBuf<uint8_t> d_lone;  // the lone-block decoder's tables and words
 	hipStream_t side = nullptr;  // the block checksum, beside the fast decode
 	hipEvent_t ev_in = nullptr;
 
@@ -685,15 +686,21 @@ struct lz4ada_decompressor {
 			host_xxh32_update(hash_all, buf + first, size_t(nout));
 	}
 
-	// A lone block is latency-bound: the 512-lane workgroup decoder (blocks
-	// it declines are redone by the two-wave decoder) decodes a 4 MiB block
-	// ~1.6x sooner than the two-wave decoder (tools/facade_time.py).
+	// A lone block is latency-bound: the lone-block decoder (every step
+	// parallel over the block's bytes, lz4ada_lone.hip) decodes a 4 MiB
+	// block ~25x sooner than the 512-lane workgroup decoder, which in turn
+	// beats the two-wave one (tools/lone_time.py, tools/facade_time.py).
+	// Below LONE_MIN compressed bytes the workgroup decoder's single launch
+	// wins.  LZ4ADA_FACADE_DECODER=wg / pc picks the others.
+	static constexpr int64_t LONE_MIN = 16 << 10;
 	static int facade_variant()
 	{
 		const char* e = getenv("LZ4ADA_FACADE_DECODER");
 		if (e && !strcmp(e, "pc"))
 			return DEC_PC;
-		return DEC_WG;
+		if (e && !strcmp(e, "wg"))
+			return DEC_WG;
+		return -1;  // lone (large blocks), else wg
 	}
 
 	// Decompress_Full_Block through the bulk decoder for one block, into a
@@ -720,9 +727,16 @@ struct lz4ada_decompressor {
 		d.flags = m.is_compressed ? 0u : LZ4ADA_BLOCK_STORED;
 		d.out_off = 0;
 		d.out_cap = uint32_t(cap);
+		const int fv = facade_variant();
+		if (fv < 0 && m.is_compressed && raw_len >= LONE_MIN) {
+			const int64_t sb = lone_scratch_bytes(raw_len, cap);
+			d_lone.reserve(size_t(sb));
+			HIP_OK(launch_decode_lone(d_blk.p, raw_len, d_scr.p, cap, d_bst.p, d_lone.p, sb, stream));
+			return start;
+		}
 		HIP_OK(hipMemcpyAsync(d_desc.p, &d, sizeof d, hipMemcpyHostToDevice, stream));
 		HIP_OK(launch_decode_variant(d_blk.p, uint64_t(std::max<int64_t>(blen, 1)), d_desc.p, 1,
-		                             d_scr.p, d_bst.p, facade_variant(), stream));
+		                             d_scr.p, d_bst.p, fv < 0 ? int(DEC_WG) : fv, stream));
 		return start;
 	}
 
@@ -2000,6 +2014,19 @@ int lz4ada_launch_decode_wg(const void* d_frame, uint64_t frame_len,
 		HIP_OK(launch_decode_wg(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
 		                        uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,
 		                        static_cast<hipStream_t>(stream)));
+	});
+}
+
+int64_t lz4ada_lone_scratch_bytes(int64_t n, int64_t cap) { return lone_scratch_bytes(n, cap); }
+
+int lz4ada_launch_decode_lone(const void* d_blk, int64_t n, void* d_out, int64_t cap,
+                              lz4ada_block_status* d_status, void* d_scratch,
+                              int64_t scratch_bytes, void* stream)
+{
+	return guarded(nullptr, [&] {
+		HIP_OK(launch_decode_lone(static_cast<const uint8_t*>(d_blk), n, static_cast<uint8_t*>(d_out),
+		                          cap, d_status, d_scratch, scratch_bytes,
+		                          static_cast<hipStream_t>(stream)));
 	});
 }
 

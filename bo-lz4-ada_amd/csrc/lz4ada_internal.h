@@ -45,7 +45,7 @@ enum DevStatus : int32_t {
 	DS_BACKREF = 7,        // lz4ada.adb:867-874 (detail = H_Offset)
 	DS_CONTENT_SIZE = 8,   // lz4ada.adb:830-835
 	DS_INTERNAL = 9,       // decoder invariant broken (never expected)
-	DS_RETRY = 10,         // k_decode_wg declined the block: k_decode_blocks redoes it
+	DS_RETRY = 10,         // a fast decoder declined the block: k_decode_pc (or the exact path) redoes it
 	DS_SPARSE = 11,        // pass 1 declined a literal-heavy block: k_decode_sparse takes it
 	                       // (k_decode_pc, retry_only, takes it like DS_RETRY)
 };
@@ -175,6 +175,14 @@ hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail
                             uint8_t* d_tail_new, hipStream_t stream);
 
 // Gather variable-length slots into a contiguous buffer (short blocks).
+// One block decoded by the whole GPU (lz4ada_lone.hip): d_st gets DS_OK and
+// out_len, or DS_RETRY (the exact path then decides).  d_scratch holds
+// lone_scratch_bytes(n, cap) bytes.
+int64_t lone_scratch_bytes(int64_t n, int64_t cap);
+hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
+                              lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
+                              hipStream_t stream);
+
 // host side (lz4ada_host.cpp): the calling thread's message for
 // lz4ada_thread_last_error() and its lz4ada_last_path() bits
 void set_thread_error(const std::string& msg);

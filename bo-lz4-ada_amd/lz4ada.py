@@ -212,6 +212,8 @@ _sig = {
     "lz4ada_decode_frame_multi_gather": ([_vp, _i64, ctypes.c_int, _P(ctypes.c_int), _vp, _i64,
                                           _pi64, _pi64], ctypes.c_int),
     "lz4ada_plan_shards": ([_vp, _i64, ctypes.c_int, _pi64], ctypes.c_int),
+    "lz4ada_lone_scratch_bytes": ([_i64, _i64], _i64),
+    "lz4ada_launch_decode_lone": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lz4ada_gen_block": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _vp, _i64], _i64),
     "lz4ada_gen_block_linked": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _i64, _vp, _i64], _i64),
 }
@@ -514,6 +516,16 @@ def launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stre
     """Workgroup-per-block decoder alone; declined blocks keep status DS_RETRY."""
     _check(_lib.lz4ada_launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status,
                                         stream), _thread_error())
+
+
+def lone_scratch_bytes(n: int, cap: int) -> int:
+    return _lib.lz4ada_lone_scratch_bytes(n, cap)
+
+
+def launch_decode_lone(d_blk, n, d_out, cap, d_status, d_scratch, scratch_bytes, stream=0):
+    """One block by the whole GPU (lz4ada_lone.hip); status DS_OK or DS_RETRY."""
+    _check(_lib.lz4ada_launch_decode_lone(d_blk, n, d_out, cap, d_status, d_scratch,
+                                          scratch_bytes, stream), _thread_error())
 
 
 DS_RETRY = 10

@@ -249,6 +249,19 @@ int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                                  lz4ada_block_status *d_status, int variant, void *stream);
 
+/* One block (payload d_blk, n bytes, no history) decoded by the whole GPU
+ * (lz4ada_lone.hip: every byte position parsed, the sequence chain found by
+ * pointer jumping, copies resolved by pointer jumping over one word per
+ * output byte) into d_out (cap bytes); *d_status gets code 0 and out_len, or
+ * 10 (declined: malformed data, a reference before the block start, an
+ * output over cap -- the exact path gives the reference's result).  The
+ * streaming facade's decoder for lone blocks.  d_scratch: device memory of
+ * lz4ada_lone_scratch_bytes(n, cap) bytes.  Asynchronous on stream. */
+int64_t lz4ada_lone_scratch_bytes(int64_t n, int64_t cap);
+int lz4ada_launch_decode_lone(const void *d_blk, int64_t n, void *d_out, int64_t cap,
+                              lz4ada_block_status *d_status, void *d_scratch,
+                              int64_t scratch_bytes, void *stream);
+
 /* The workgroup-per-block decoder alone: blocks it declines (malformed
  * data, oversize sequences) keep status code 10 (retry) and are not
  * decoded; lz4ada_launch_decode runs it and then redoes those blocks. */

@@ -1,0 +1,103 @@
+"""The lone-block decoder (lz4ada_lone.hip: one block by the whole GPU, the
+streaming facade's decoder) against the generator's bytes and the CPU
+oracle's block decode (oracle/lz4ada_oracle.c, lz4ada.adb:716-904): every
+block it accepts is byte-exact; anything the reference would reject or that
+reads before the block start is declined (status 10), never decoded
+differently."""
+import ctypes
+import random
+
+import pytest
+
+import _oracle as O
+from _lz4build import encode, sparse_seqs
+
+import lz4ada
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not lz4ada.device_available():
+        pytest.fail("MI355X not usable: " + lz4ada._thread_error())
+
+
+def run_lone(comp, cap):
+    import torch
+    n = len(comp)
+    d_in = torch.frombuffer(bytearray(comp + b"\0" * 16), dtype=torch.uint8).cuda()
+    d_out = torch.zeros(max(cap, 1), dtype=torch.uint8, device="cuda")
+    d_st = torch.zeros(ctypes.sizeof(lz4ada.BlockStatus), dtype=torch.uint8, device="cuda")
+    sb = lz4ada.lone_scratch_bytes(n, cap)
+    d_sc = torch.empty(sb, dtype=torch.uint8, device="cuda")
+    lz4ada.launch_decode_lone(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_st.data_ptr(),
+                              d_sc.data_ptr(), sb, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    st = lz4ada.BlockStatus.from_buffer_copy(d_st.cpu().numpy().tobytes())
+    return st, d_out[:st.out_len].cpu().numpy().tobytes() if st.code == 0 else b""
+
+
+def oracle_block(comp, cap):
+    """(ok, bytes) of the reference decoding comp as one raw block."""
+    ctx = O.Decompressor.init_for_block(len(comp))
+    buf = ctypes.create_string_buffer(ctx.min_buffer_size)
+    st, c, f, l = ctx.update(comp, buf)
+    if st != O.OK:
+        return False, b""
+    out = buf.raw[f:l + 1] if l >= f else b""
+    return len(out) <= cap, out
+
+
+@pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
+@pytest.mark.parametrize("size", [1, 13, 100, 4095, 4096, 4097, 65536, 300001, 1 << 20, 4 << 20])
+def test_lone_generated_blocks(kind, size):
+    comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 0x10E + size, size)
+    st, out = run_lone(comp, 4 << 20)
+    assert st.code == 0, st.code
+    assert st.out_len == len(raw)
+    assert out == raw
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_lone_long_literals_and_matches(seed):
+    """Runs longer than a 4 KiB window (a sequence jumping over windows),
+    one-byte and multi-byte length extensions, overlapping matches."""
+    rng = random.Random(seed)
+    seqs = sparse_seqs(rng, 3 << 20, lit_lo=1, lit_hi=20000,
+                       offs=[1, 2, 3, 7, 16, 100, 5000, 60000], mls=[4, 18, 19, 300, 70000])
+    comp, raw = encode(seqs, final_lits=rng.randbytes(rng.choice([0, 5, 40])))
+    st, out = run_lone(comp, 4 << 20)
+    assert st.code == 0, st.code
+    assert out == raw
+
+
+def test_lone_output_over_cap_declines():
+    comp, raw = lz4ada.gen_block(lz4ada.GEN_MIXED, 5, 1 << 20)
+    st, _ = run_lone(comp, len(raw) - 1)
+    assert st.code == lz4ada.DS_RETRY
+    st, out = run_lone(comp, len(raw))
+    assert st.code == 0 and out == raw
+
+
+def test_lone_reference_before_block_start_declines():
+    blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_MIXED, 3, 0, 0, lens=[65536, 65536])
+    st, _ = run_lone(blocks[1][0], 1 << 20)
+    assert st.code == lz4ada.DS_RETRY
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_lone_corrupted_blocks_never_differ(seed):
+    rng = random.Random(seed)
+    comp, raw = lz4ada.gen_block(seed % 4, 77 + seed, rng.choice([5000, 70000, 300000]))
+    b = bytearray(comp)
+    for _ in range(rng.randrange(1, 4)):
+        b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+    if seed % 5 == 0:
+        b = b[:rng.randrange(1, len(b))]
+    cap = 1 << 20
+    ok, ref = oracle_block(bytes(b), cap)
+    st, out = run_lone(bytes(b), cap)
+    assert st.code in (0, lz4ada.DS_RETRY)
+    if st.code == 0:
+        assert ok and out == ref
