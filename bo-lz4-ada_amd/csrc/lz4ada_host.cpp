@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <future>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -405,6 +406,16 @@ struct lz4ada_decompressor {
 	int64_t d_buf_len = 0;
 	DevBuf<uint8_t> d_blk;
 	lz4ada_xxh32_state hash_all{};  // Hash_All_Data, over the bytes the GPU decoded
+	// A large block's content hash runs on a helper thread while the caller
+	// feeds the next block (the caller's Buffer is not modified between
+	// calls); every reader of hash_all joins it first.
+	std::future<void> hash_job;
+	void hash_wait()
+	{
+		if (hash_job.valid())
+			hash_job.get();
+	}
+	std::vector<uint8_t> blk_tmp;  // a block assembled from cached + new input
 	DevBuf<lz4ada_xxh32_state> d_tmp_hash;
 	DevBuf<SerialState> d_serial;
 	DevBuf<lz4ada_block_desc> d_desc;  // one-block fast path
@@ -437,6 +448,8 @@ struct lz4ada_decompressor {
 	lz4ada_decompressor() { lz4ada_xxh32_reset(&hash_all, 0); }
 	~lz4ada_decompressor()
 	{
+		if (hash_job.valid())
+			hash_job.wait();
 		if (side) {
 			(void)hipStreamSynchronize(side);
 			(void)hipStreamDestroy(side);
@@ -465,7 +478,11 @@ struct lz4ada_decompressor {
 		dev_ready = true;
 	}
 
-	void reset_content_hash() { lz4ada_xxh32_reset(&hash_all, 0); }  // XXHash32.Reset(0)
+	void reset_content_hash()  // XXHash32.Reset(0)
+	{
+		hash_wait();
+		lz4ada_xxh32_reset(&hash_all, 0);
+	}
 
 	// ---------------------------------------------------- Update pieces
 	void reset_outer()  // lz4ada.adb:451-461
@@ -512,7 +529,11 @@ struct lz4ada_decompressor {
 			              img_u(m.size_remaining) + " bytes left to output.");
 	}
 
-	uint32_t content_hash_final() { return host_xxh32_final(hash_all); }
+	uint32_t content_hash_final()
+	{
+		hash_wait();
+		return host_xxh32_final(hash_all);
+	}
 
 	void check_end_mark(const uint8_t* in, int64_t len, int64_t& consumed)  // :463-523
 	{
@@ -605,47 +626,54 @@ struct lz4ada_decompressor {
 		const int64_t raw_len = blen - bcl;
 		if (buflen > d_buf_len)
 			grow_mirror(buflen);
+		static const bool trace = getenv("LZ4ADA_TRACE_FACADE") != nullptr;
+		auto t0 = std::chrono::steady_clock::now();
+		auto phase = [&](const char* name) {
+			if (!trace)
+				return;
+			const auto t1 = std::chrono::steady_clock::now();
+			fprintf(stderr, "[facade] %-8s %8.3f ms\n", name,
+			        std::chrono::duration<double, std::milli>(t1 - t0).count());
+			t0 = t1;
+		};
 		d_blk.reserve(size_t(std::max<int64_t>(blen, 1)));
-		if (blen > 0)
-			HIP_OK(hipMemcpyAsync(d_blk.p, blk, size_t(blen), hipMemcpyHostToDevice, stream));
-		// Check_Checksum comes before decoding (:672-676, quirk Q8): the
-		// checksum (one serial chain) runs on the side stream while the fast
-		// decode writes a scratch slot, and the mirror only takes the output
-		// once the checksum has passed
-		lz4ada_xxh32_state h;
-		if (bcl > 0) {
+		// Check_Checksum comes before decoding (:672-676, quirk Q8).  The
+		// payload is host memory here: its XXH32 runs on this thread (one
+		// serial chain, ~10x the GPU chain's rate) while the GPU decodes
+		// into a scratch slot; the mirror takes the output only once the
+		// checksum has passed.  A block known to fail (the bulk path stopped
+		// at it) is checked before anything is launched.
+		auto check = [&] {
+			lz4ada_xxh32_state h;
 			lz4ada_xxh32_reset(&h, 0);
-			HIP_OK(hipMemcpyAsync(d_tmp_hash.p, &h, sizeof h, hipMemcpyHostToDevice, stream));
-			HIP_OK(hipEventRecord(ev_in, stream));
-			HIP_OK(hipStreamWaitEvent(side, ev_in, 0));
-			HIP_OK(launch_xxh32_update(d_tmp_hash.p, d_blk.p, uint64_t(raw_len), side));
-		}
+			host_xxh32_update(h, blk, size_t(raw_len));
+			const uint32_t got = host_xxh32_final(h);
+			const uint32_t expect = load32(blk + blen - bcl);
+			return std::make_pair(got == expect, "Declared checksum is 0x" + hex32(expect) +
+			                                             ", but computed one is 0x" + hex32(got) + ".");
+		};
 		if (checksum_first && bcl > 0) {
 			checksum_first = false;
-			HIP_OK(hipMemcpyAsync(&h, d_tmp_hash.p, sizeof h, hipMemcpyDeviceToHost, side));
-			HIP_OK(hipStreamSynchronize(side));
-			const uint32_t expect = load32(blk + blen - bcl);
-			if (h.hash != expect)
-				raise(LZ4ADA_CHECKSUM_ERROR, "Declared checksum is 0x" + hex32(expect) +
-				                                     ", but computed one is 0x" + hex32(h.hash) +
-				                                     ".");
+			const auto c = check();
+			if (!c.first)
+				raise(LZ4ADA_CHECKSUM_ERROR, c.second);
 		}
+		if (blen > 0)
+			HIP_OK(hipMemcpyAsync(d_blk.p, blk, size_t(blen), hipMemcpyHostToDevice, stream));
+		phase("h2d");
 		const int64_t fast_start = launch_fast_block(raw_len, blen, buflen);
 		if (bcl > 0) {
-			// after the decode launch: a copy into pageable memory returns
-			// only once it is done
-			HIP_OK(hipMemcpyAsync(&h, d_tmp_hash.p, sizeof h, hipMemcpyDeviceToHost, side));
-			HIP_OK(hipStreamSynchronize(side));
-			const uint32_t expect = load32(blk + blen - bcl);
-			if (h.hash != expect) {
+			const auto c = check();
+			phase("cksum");
+			if (!c.first) {
 				HIP_OK(hipStreamSynchronize(stream));  // the scratch decode, discarded
-				raise(LZ4ADA_CHECKSUM_ERROR, "Declared checksum is 0x" + hex32(expect) +
-				                                     ", but computed one is 0x" + hex32(h.hash) +
-				                                     ".");
+				raise(LZ4ADA_CHECKSUM_ERROR, c.second);
 			}
 		}
 		if (fast_start >= 0 && finish_fast_block(fast_start, first, last)) {
+			phase("decode");
 			deliver(buf, first, last);
+			phase("deliver");
 			return;
 		}
 		SerialState s{};
@@ -679,11 +707,26 @@ struct lz4ada_decompressor {
 		const int64_t nout = last - first + 1;
 		if (nout <= 0)
 			return;
+		static const bool trace = getenv("LZ4ADA_TRACE_FACADE") != nullptr;
+		const auto t0 = std::chrono::steady_clock::now();
+		hash_wait();  // the previous block's bytes may share this Buffer range
 		HIP_OK(hipMemcpyAsync(buf + first, d_buf.p + first, size_t(nout), hipMemcpyDeviceToHost,
 		                      stream));
 		HIP_OK(hipStreamSynchronize(stream));
-		if (m.content_checksum_length != 0)
-			host_xxh32_update(hash_all, buf + first, size_t(nout));
+		const auto t1 = std::chrono::steady_clock::now();
+		if (m.content_checksum_length != 0) {
+			const uint8_t* p = buf + first;
+			if (nout >= (int64_t(256) << 10))
+				hash_job = std::async(std::launch::async,
+				                      [this, p, nout] { host_xxh32_update(hash_all, p, size_t(nout)); });
+			else
+				host_xxh32_update(hash_all, p, size_t(nout));
+		}
+		if (trace)
+			fprintf(stderr, "[facade]   d2h %.3f ms, content hash %.3f ms\n",
+			        std::chrono::duration<double, std::milli>(t1 - t0).count(),
+			        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1)
+			                .count());
 	}
 
 	// A lone block is latency-bound: the lone-block decoder (every step
@@ -873,7 +916,10 @@ struct lz4ada_decompressor {
 			HIP_OK(hipMemcpyAsync(buf + start, src, size_t(nout), hipMemcpyDeviceToHost, stream));
 			HIP_OK(hipStreamSynchronize(stream));
 			if (m.content_checksum_length != 0)
-				host_xxh32_update(hash_all, buf + start, size_t(nout));
+			{
+			hash_wait();
+			host_xxh32_update(hash_all, buf + start, size_t(nout));
+		}
 		}
 		if (m.has_content_size)
 			m.size_remaining -= uint64_t(nout);
@@ -906,11 +952,18 @@ struct lz4ada_decompressor {
 			// Input_Buffer(4 .. Fill-1) & Input(...): drops 4 cached bytes for
 			// the raw-block format (quirk Q5), like the reference.
 			const int64_t head = std::max<int64_t>(fill - BLOCK_SIZE_BYTES, 0);
-			std::vector<uint8_t> blk(size_t(head + want));
+			if (fill >= BLOCK_SIZE_BYTES && fill + want <= int64_t(input_buffer.size())) {
+				// the rest of the block right after the cached bytes: no copy
+				memcpy(input_buffer.data() + fill, src, size_t(want));
+				decode_full_block(input_buffer.data() + BLOCK_SIZE_BYTES, head + want, buf, buflen,
+				                  first, last);
+				return;
+			}
+			blk_tmp.resize(size_t(head + want));
 			if (head)
-				memcpy(blk.data(), input_buffer.data() + BLOCK_SIZE_BYTES, size_t(head));
-			memcpy(blk.data() + head, src, size_t(want));
-			decode_full_block(blk.data(), head + want, buf, buflen, first, last);
+				memcpy(blk_tmp.data(), input_buffer.data() + BLOCK_SIZE_BYTES, size_t(head));
+			memcpy(blk_tmp.data() + head, src, size_t(want));
+			decode_full_block(blk_tmp.data(), head + want, buf, buflen, first, last);
 		}
 	}
 

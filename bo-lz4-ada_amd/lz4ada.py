@@ -37,6 +37,15 @@ if not os.path.exists(LIB_PATH):
 
 _lib = ctypes.CDLL(LIB_PATH)
 
+# Decompressor.update through the CPython module (csrc/pyfast.c: no ctypes
+# conversion per call) when it binds this same library.
+_fast = None
+if not os.environ.get("LZ4ADA_LIB") and not os.environ.get("LZ4ADA_NO_PYFAST"):
+    try:
+        import _lz4ada_fast as _fast  # noqa: E402  (bo-lz4-ada_amd/ is on sys.path)
+    except ImportError:
+        _fast = None
+
 _i64 = ctypes.c_int64
 _pi64 = ctypes.POINTER(ctypes.c_int64)
 _vp = ctypes.c_void_p
@@ -268,10 +277,16 @@ class Decompressor:
 
     def __init__(self, ptr: int):
         self._p = _vp(ptr)
+        # per-call ctypes objects made once (an Update loop calls this once
+        # per 4 KiB read: unlz4ada.adb:84-103)
+        self._out = (_i64(), _i64(), _i64())
+        self._refs = tuple(ctypes.byref(x) for x in self._out)
+        self._data = self._data_addr = None
+        self._buf = self._buf_view = None
 
     def __del__(self):
         p = getattr(self, "_p", None)
-        if p is not None and p.value:
+        if p is not None and p.value and _lib is not None:
             _lib.lz4ada_free(p)
             self._p = None
 
@@ -304,11 +319,27 @@ class Decompressor:
         """Update (lz4ada.ads:281-287) on data[start:stop] ->
         (num_consumed, output_first, output_last); output is buffer[first:last+1]."""
         stop = len(data) if stop is None else stop
+        if _fast is not None and isinstance(buffer, bytearray):
+            st, c, f, l = _fast.update(self._p.value, data, start, stop, buffer)
+            if st:
+                _check(st, _lib.lz4ada_last_error(self._p).decode())
+            return c, f, l
         n = stop - start
-        cons, first, last = _i64(), _i64(), _i64()
-        st = _lib.lz4ada_update(self._p, _addr(data, start) if n > 0 else None, n,
-                                ctypes.byref(cons), _addr(buffer), len(buffer),
-                                ctypes.byref(first), ctypes.byref(last))
+        cons, first, last = self._out
+        rc, rf, rl = self._refs
+        if data is not self._data:  # the same input object: its address is kept
+            self._data = data
+            self._data_addr = _addr(data) if isinstance(data, bytes) else None
+        src = (self._data_addr + start if self._data_addr is not None else _addr(data, start)) \
+            if n > 0 else None
+        if buffer is not self._buf:
+            # a ctypes view pins the bytearray (no resize while this context
+            # holds it), so its address can be kept
+            self._buf = buffer
+            self._buf_view = (ctypes.c_char * len(buffer)).from_buffer(buffer) \
+                if isinstance(buffer, bytearray) and len(buffer) else None
+        dst = self._buf_view if self._buf_view is not None else _addr(buffer)
+        st = _lib.lz4ada_update(self._p, src, n, rc, dst, len(buffer), rf, rl)
         if st:
             _check(st, _lib.lz4ada_last_error(self._p).decode())
         return cons.value, first.value, last.value
