@@ -385,6 +385,27 @@ using namespace lz4ada;
 
 // ----------------------------------------------------------- Decompressor
 
+namespace lz4ada {
+// A few large blocks: one block at a time through the lone-block decoder
+// (lz4ada_lone.hip, the whole GPU per block: ~0.4 ms per 4 MiB mixed block)
+// beats the bulk decoder's one wave per block (~13 ms per 4 MiB block, at
+// any count up to the chip's 2,048 resident waves) below ~30 blocks.
+static bool few_large_blocks(const std::vector<lz4ada_block_desc>& d)
+{
+	static const bool off = getenv("LZ4ADA_NO_LONE") != nullptr;
+	if (off || d.empty() || d.size() > 24)
+		return false;
+	uint32_t mx = 0;
+	for (const auto& x : d)
+		mx = std::max(mx, x.in_len);
+	return mx >= (512u << 10);
+}
+static bool decode_lone_blocks(const uint8_t* host_in, const uint8_t* d_in,
+                               const std::vector<lz4ada_block_desc>& d, uint8_t* d_out,
+                               lz4ada_block_status* d_st, std::vector<lz4ada_block_status>& st,
+                               DevBuf<uint8_t>& scr, hipStream_t stream);
+}  // namespace lz4ada
+
 struct lz4ada_decompressor {
 	Meta m;
 	bool is_at_end_mark = false;
@@ -432,7 +453,7 @@ struct lz4ada_decompressor {
 		std::vector<uint8_t> input;  // the batch's compressed bytes (identity check)
 		std::vector<lz4ada_block_desc> descs;
 		std::vector<lz4ada_block_status> st;
-		DevBuf<uint8_t> d_in, d_out;
+		DevBuf<uint8_t> d_in, d_out, d_lone;
 		DevBuf<lz4ada_block_desc> d_desc;
 		DevBuf<lz4ada_block_status> d_st;
 		uint64_t slot = 0;
@@ -866,6 +887,11 @@ struct lz4ada_decompressor {
 		HIP_OK(hipMemcpyAsync(ahead.d_in.p, blk, size_t(pos), hipMemcpyHostToDevice, stream));
 		HIP_OK(hipMemcpyAsync(ahead.d_desc.p, ahead.descs.data(), nb * sizeof(lz4ada_block_desc),
 		                      hipMemcpyHostToDevice, stream));
+		HIP_OK(hipMemsetAsync(ahead.d_st.p, 0, nb * sizeof(lz4ada_block_status), stream));
+		if (few_large_blocks(ahead.descs) &&
+		    decode_lone_blocks(blk, ahead.d_in.p, ahead.descs, ahead.d_out.p, ahead.d_st.p, ahead.st,
+		                       ahead.d_lone, stream))
+			return true;
 		HIP_OK(hipMemsetAsync(ahead.d_st.p, 0, nb * sizeof(lz4ada_block_status), stream));
 		if (bcl)
 			HIP_OK(launch_block_checksums(ahead.d_in.p, ahead.d_desc.p, uint32_t(nb), ahead.d_st.p,
@@ -1525,7 +1551,7 @@ static bool try_reserve(DevBuf<T>& b, size_t count)
 // and a first-touch each time otherwise -- more than the decode itself on a
 // 1 GiB linked frame.  lz4ada_release_device_cache() frees them.  The
 // cache is never destroyed at thread exit (the HIP runtime may be gone).
-enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_TAB, SC_P, SC_F, SC_N };
+enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_TAB, SC_P, SC_F, SC_LONE, SC_N };
 struct ScratchCache {
 	DevBuf<uint8_t> b[SC_N];
 };
@@ -1555,6 +1581,75 @@ static int64_t env_bytes(const char* name, int64_t dflt)
 		return dflt;
 	const long long v = atoll(e);
 	return v > 0 ? int64_t(v) : dflt;
+}
+
+// decode_lone_blocks: every block of d (host descriptors, offsets into d_in
+// and d_out) through the lone-block decoder, stored ones as a copy, while
+// host threads hash the blocks' host bytes for their checksums
+// (lz4ada.adb:698-707).  st gets code, out_len and cksum as the bulk
+// decoder's statuses carry them; false when a block was declined (the
+// caller then runs the bulk decoder, which produces the exact status).
+static bool decode_lone_blocks(const uint8_t* host_in, const uint8_t* d_in,
+                               const std::vector<lz4ada_block_desc>& d, uint8_t* d_out,
+                               lz4ada_block_status* d_st, std::vector<lz4ada_block_status>& st,
+                               DevBuf<uint8_t>& scr, hipStream_t stream)
+{
+	const size_t nb = d.size();
+	int64_t sb = 0;
+	for (const auto& x : d) {
+		if (x.flags & LZ4ADA_BLOCK_STORED) {
+			if (x.in_len > x.out_cap)
+				return false;
+		} else {
+			if (x.in_len == 0)
+				return false;
+			sb = std::max(sb, lone_scratch_bytes(x.in_len, x.out_cap));
+		}
+	}
+	if (sb && !try_reserve(scr, size_t(sb)))
+		return false;
+	HIP_OK(hipMemsetAsync(d_st, 0, nb * sizeof(lz4ada_block_status), stream));
+	for (size_t i = 0; i < nb; ++i) {
+		const auto& x = d[i];
+		if (x.flags & LZ4ADA_BLOCK_STORED) {
+			if (x.in_len)
+				HIP_OK(hipMemcpyAsync(d_out + x.out_off, d_in + x.in_off, x.in_len,
+				                      hipMemcpyDeviceToDevice, stream));
+		} else {
+			HIP_OK(launch_decode_lone(d_in + x.in_off, x.in_len, d_out + x.out_off, x.out_cap,
+			                          d_st + i, scr.p, sb, stream));
+		}
+	}
+	std::vector<std::future<uint32_t>> ck(nb);
+	for (size_t i = 0; i < nb; ++i)
+		if (d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) {
+			const uint8_t* p = host_in + d[i].in_off;
+			const size_t n = d[i].in_len;
+			ck[i] = std::async(std::launch::async, [p, n] {
+				lz4ada_xxh32_state h;
+				lz4ada_xxh32_reset(&h, 0);
+				host_xxh32_update(h, p, n);
+				return host_xxh32_final(h);
+			});
+		}
+	st.assign(nb, lz4ada_block_status{});
+	HIP_OK(hipMemcpyAsync(st.data(), d_st, nb * sizeof(lz4ada_block_status), hipMemcpyDeviceToHost,
+	                      stream));
+	HIP_OK(hipStreamSynchronize(stream));
+	bool ok = true;
+	for (size_t i = 0; i < nb; ++i) {
+		if (d[i].flags & LZ4ADA_BLOCK_STORED) {
+			st[i].code = DS_OK;
+			st[i].out_len = d[i].in_len;
+		}
+		if (ck[i].valid())
+			st[i].cksum = ck[i].get();
+		if (st[i].code != DS_OK)
+			ok = false;
+	}
+	if (ok)  // the statuses also on the device, as the bulk decoder leaves them
+		HIP_OK(hipMemcpy(d_st, st.data(), nb * sizeof(lz4ada_block_status), hipMemcpyHostToDevice));
+	return ok;
 }
 
 // Output slot capacity of one block: a stored block is its payload; a
@@ -1601,7 +1696,8 @@ enum BulkResult { BULK_OK, BULK_EXACT, BULK_PRE_REF, BULK_FAIL_AT };
 // BULK_FAIL_AT: block `fail` has a bad status or checksum; the blocks before
 // it are committed (their lengths in `lens`), so the exact path can resume
 // there instead of redoing the frame.
-static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_info& info,
+static BulkResult bulk_independent(const uint8_t* d_frame, const uint8_t* host_frame,
+                                   const lz4ada_frame_info& info,
                                    const std::vector<lz4ada_block_desc>& descs, Sink& out,
                                    lz4ada_xxh32_state* h, uint64_t& total,
                                    std::vector<uint32_t>& lens, int64_t& fail)
@@ -1637,11 +1733,16 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const lz4ada_frame_in
 		d_desc.reserve(nb);
 		d_st.reserve(nb);
 		HIP_OK(hipMemcpy(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc), hipMemcpyHostToDevice));
-		HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
-		HIP_OK(launch_decode_checked(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out, d_st.p,
-		                             stream));
 		std::vector<lz4ada_block_status> st(nb);
-		HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status), hipMemcpyDeviceToHost));
+		if (!(host_frame && few_large_blocks(d) &&
+		      decode_lone_blocks(host_frame, d_frame, d, d_out, d_st.p, st,
+		                         scratch_cache().b[SC_LONE], stream))) {
+			HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
+			HIP_OK(launch_decode_checked(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out,
+			                             d_st.p, stream));
+			HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status),
+			                 hipMemcpyDeviceToHost));
+		}
 		uint64_t bt_total = 0;
 		bool contiguous = true;
 		std::vector<uint64_t> dst_off(nb);
@@ -1956,7 +2057,7 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 			std::vector<uint32_t> lens;
 			int64_t fail = -1;
 			if (info.independent && !getenv("LZ4ADA_FORCE_LINKED"))
-				r = bulk_independent(d_frame.p, info, descs, out, h, total, lens, fail);
+				r = bulk_independent(d_frame.p, f, info, descs, out, h, total, lens, fail);
 			phase("bulk");
 			const bool linked = r == BULK_PRE_REF;
 			if (linked) {

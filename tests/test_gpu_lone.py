@@ -101,3 +101,57 @@ def test_lone_corrupted_blocks_never_differ(seed):
     assert st.code in (0, lz4ada.DS_RETRY)
     if st.code == 0:
         assert ok and out == ref
+
+
+# ------------------------------------------- frames of a few large blocks
+# (lz4ada_host.cpp few_large_blocks: decode_frame and the facade's read-ahead
+# take such frames one block at a time through the lone-block decoder)
+
+def few_block_frame(kinds, seed=9, stored_at=None):
+    import lz4frame
+    blocks = []
+    for i, k in enumerate(kinds):
+        if i == stored_at:
+            raw = random.Random(seed + i).randbytes(3 << 20)
+            blocks.append((raw, raw, True))
+        else:
+            comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[k], seed * 100 + i, 4 << 20)
+            blocks.append((comp, raw, False))
+    return lz4frame.build_frame(blocks, 4 << 20, indep=True, block_cksum=True, content_cksum=True)
+
+
+@pytest.mark.parametrize("kinds,stored_at", [
+    (["mixed"] * 5, None),
+    (["literal", "dense", "mixed", "rle"], 2),
+])
+def test_few_large_blocks_decode_frame(kinds, stored_at):
+    frame, raw = few_block_frame(kinds, stored_at=stored_at)
+    out, cons = lz4ada.decode_frame(frame)
+    assert out == raw and cons == len(frame)
+    assert lz4ada.last_path() == lz4ada.PATH_INDEPENDENT
+
+
+def test_few_large_blocks_bad_checksum_is_the_references():
+    frame, raw = few_block_frame(["mixed"] * 4)
+    info, descs = lz4ada.frame_index(frame)
+    b = bytearray(frame)
+    b[descs[2].in_off + 999] ^= 4
+    st, ref, msg = O.unlz4ada(bytes(b), out_cap=len(raw) + (1 << 20))
+    out, cons, exc = lz4ada.decode_frame_partial(bytes(b))
+    assert exc is not None and str(exc) == O.exception_information(st, msg)
+    assert out == ref
+
+
+def test_few_large_blocks_facade_read_ahead():
+    frame, raw = few_block_frame(["mixed", "dense", "literal"])
+    ctx, used, mbs = lz4ada.Decompressor.init_with_header(frame)
+    buf = bytearray(mbs)
+    out, pos = bytearray(), used
+    while pos < len(frame):
+        c, f, l = ctx.update(frame, buf, pos)  # all remaining input each call
+        if l >= f:
+            out += buf[f:l + 1]
+        pos += c
+        if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
+            break
+    assert bytes(out) == raw

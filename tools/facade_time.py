@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--indep", type=int, default=1)
     ap.add_argument("--bcksum", type=int, default=1, help="block checksums in the frame")
     ap.add_argument("--ccksum", type=int, default=1, help="content checksum in the frame")
+    ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     blocks = []
     for i in range(args.blocks):
@@ -52,10 +53,12 @@ def main():
                                          block_cksum=bool(args.bcksum),
                                           content_cksum=bool(args.ccksum))
     run(frame, expect, args.feed)  # warm
-    dt = run(frame, expect, args.feed)
+    ts = sorted(run(frame, expect, args.feed) for _ in range(args.reps))
+    dt = ts[len(ts) // 2]
     print(f"facade {args.kind} feed={args.feed} bcksum={args.bcksum} ccksum={args.ccksum} "
-          f"{args.blocks}x{args.block_max >> 10} KiB: "
-          f"{dt * 1e3:.1f} ms  {len(expect) / dt / 2**20:.1f} MiB/s")
+          f"{args.blocks}x{args.block_max >> 10} KiB: median of {args.reps} "
+          f"{dt * 1e3:.1f} ms  {len(expect) / dt / 2**20:.1f} MiB/s "
+          f"(best {len(expect) / ts[0] / 2**20:.1f}, worst {len(expect) / ts[-1] / 2**20:.1f})")
 
 
 if __name__ == "__main__":

@@ -14,6 +14,7 @@ os.environ.setdefault("LZ4ADA_LIB", os.path.join(ROOT, "bo-lz4-ada_amd", "_varia
                                                   "liblz4ada_hip_idxst.so"))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "bo-lz4-ada_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -37,8 +38,11 @@ def main():
     f.argtypes = [ctypes.c_void_p, ctypes.c_int]
     buf = (ctypes.c_ulonglong * len(NAMES))()
     for kind in args.kinds.split(","):
-        recs = bench.make_unique_blocks(lz4ada.GEN_KINDS[kind], 64, bmax)
-        fr, fl, de, eh, cb, rb, _ = bench.build_shard(recs, 0, args.blocks, bmax, dev)
+        import lz4frame
+        import xxhash
+        recs = bench.make_unique_blocks(lz4ada, lz4frame, xxhash, kind, 64, bmax)
+        fr, fl, de, eh, cb, rb, _ = bench.assemble_shard(lz4ada, torch, recs, 0, args.blocks, bmax,
+                                                         dev)
         out = torch.empty(args.blocks * bmax, dtype=torch.uint8, device=dev)
         st = torch.zeros(args.blocks * 32, dtype=torch.uint8, device=dev)
         sh = torch.cuda.current_stream(dev).cuda_stream
