@@ -387,6 +387,21 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
 		}
 		if (!__syncthreads_or(ch) || it > uint32_t(nwin) + 2)
 			break;
+		// still changing after two passes: the guesses are poor (sequences
+		// too far apart for speculative chains to merge, e.g. long literal
+		// runs).  Entries 0..it are exact; one lane walks the rest, one
+		// dependent lookup per window instead of one pass per window, and
+		// the next pass confirms.
+		if (it == 2) {
+			if (tid == 0) {
+				for (int32_t w = int32_t(it); w < nwin; ++w) {
+					const uint32_t e = E[w];
+					const uint32_t lim = uint32_t(min((w + 1) * LW, n));
+					E[w + 1] = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
+				}
+			}
+			__syncthreads();
+		}
 	}
 	// each window's output bytes along the chain; an exclusive scan places
 	// the windows (exact in 32 bits once the 64-bit total fits the slot)
