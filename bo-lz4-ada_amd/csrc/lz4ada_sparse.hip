@@ -1,4 +1,4 @@
-// lz4ada_sparse.hip -- bulk decoder for literal-heavy ("sparse") blocks.
+// lz4ada_sparse.hip -- streaming decoder for literal-heavy ("sparse") blocks.
 //
 // Same reference path as the index decoder (lib/lz4ada.adb:716-904:
 // Decompress_Full_Block / Decompress_Sequence / Write_Output /
@@ -6,22 +6,34 @@
 // sequences are too far apart for speculative walks to merge (long literal
 // runs: incompressible text, mostly-stored content in compressed blocks).
 // Such a block holds few sequences (~9k per 4 MiB at 470 B each) and is a
-// copy job, so one wave per block:
+// copy job, so one wave per block, streaming:
 //
-//  * parse: the sequence chain walked wave-uniformly (scalar registers) over
-//    a 16 KiB LDS ring the compressed stream is staged through in 4 KiB
-//    coalesced chunks, one chunk prefetched in registers; sequence j of a
-//    batch of 64 lands in lane j's registers;
-//  * literals: groups of 8 runs, each copied by the whole wave (16 B per
-//    lane, 2 KiB per run in one step), all loads of a group issued before
-//    its stores: HBM -> HBM, no LDS;
-//  * matches: lane j runs match j of the batch once no earlier match of the
+//  * staging: the compressed stream flows through a 16 KiB LDS ring in 2 KiB
+//    chunks by LDS-DMA (global_load_lds_dwordx4, no registers), DEPTH chunks
+//    in flight ahead of the parse;
+//  * parse: the sequence chain walked wave-uniformly from the ring;
+//  * literals (Write_Output, :790-824): each run is copied the moment its
+//    sequence is parsed, from the ring to HBM (the bytes are staged anyway:
+//    the compressed stream is read from HBM once), 1 KiB per store
+//    instruction; a run longer than the staged window goes HBM -> HBM;
+//  * matches (Output_With_History, :845-904): sequence j of a batch of 64
+//    records its match in lane j; the batch's matches run at the end of the
+//    NEXT batch, when everything the batch stored has long completed, so
+//    their wait is for memory operations a whole batch old and never drains
+//    the staging stream.  Lane j runs match j once no earlier match of the
 //    batch writes a byte it reads (a dependency mask from two binary
-//    searches over the batch's monotone match positions); the source is
-//    read from the output already written (L1-bypassing loads after the
-//    wave's stores have completed); a match reads only its first `off`
-//    source bytes -- byte i is source byte i mod off -- so no piece reads
-//    its own match.
+//    searches over the batch's monotone match positions); sources are read
+//    from the output already written (L1-bypassing loads); a match reads
+//    only its first `off` source bytes -- byte i is source byte i mod off --
+//    so no piece reads its own match.
+//
+// The wave's vector-memory counter is in order, and the LDS-DMA loads are
+// invisible to the compiler's wait pass, so the waits for staged chunks and
+// for a batch's stores are counted by hand: `nvm` is a lower bound of the
+// vector-memory instructions issued so far (every DMA chunk 2, every literal
+// store round 1, every HBM copy step 2 -- a store the compiler splits only
+// adds more), and "everything issued before point X has completed" is
+// vmcnt <= nvm - nvm_at_X, rounded down to an encodable count.
 //
 // Anything unusual -- malformed data, a reference before the block start
 // (D2), a slot overflow, or a chain denser than sparse data (one sequence
@@ -37,26 +49,84 @@
 namespace lz4ada {
 namespace sparse {
 
-constexpr int STG = 2048;         // staged chunk (two LDS-DMA instructions)
-constexpr int NSLOT = 8;          // ring slots
-constexpr int RING = NSLOT * STG; // LDS ring of compressed bytes (16 KiB)
-constexpr int DEPTH = 6;          // chunks in flight ahead of the parse
-constexpr int NSEQ = 64;          // sequences per batch (one per lane)
-constexpr int OWN = 2048;         // literal pieces (16 B) dealt per batch at most
-constexpr int BIG = 4096;         // longer literal runs: copied by the whole wave
-constexpr int LONGM = 512;        // longer matches: copied by the whole wave
-constexpr int U = 8;              // pieces per lane in flight (8 KiB per wave)
-constexpr int DENSE_BYTES = 48;   // fewer input bytes per sequence: decline
+constexpr int STG = 2048;          // staged chunk (two LDS-DMA instructions)
+constexpr int NSLOT = 8;           // ring slots
+constexpr int RING = NSLOT * STG;  // LDS ring of compressed bytes (16 KiB)
+constexpr int DEPTH = 5;           // chunks in flight beyond the landed ones
+// The parse keeps [p, p + AHEAD) landed.  After a chunk is issued the ring
+// still holds the NSLOT - DEPTH chunks before the newest landed one, i.e.
+// every byte from p - (3 * STG - AHEAD - STG) on: the position being parsed
+// and everything after it stay valid while chunks are issued.
+constexpr int AHEAD = 3088;
+constexpr int NSEQ = 64;           // sequences per batch (one match per lane)
+constexpr int LONGM = 512;         // longer matches: copied by the whole wave
+constexpr int U = 8;               // HBM -> HBM copies: pieces per lane in flight (8 KiB per wave)
+constexpr int DENSE_BYTES = 48;    // fewer input bytes per sequence: decline
+static_assert(AHEAD + 2 * STG <= (NSLOT - DEPTH) * STG + STG, "parse window vs ring slack");
 
 struct alignas(16) SpLds {
-	uint8_t ring[RING];       // filled by LDS-DMA, STG-byte slots
-	uint8_t own[OWN];         // piece t's sequence: marks at run starts, prefix max
-	u32x4 rec[NSEQ];          // sequence j: src - 16 s_j, dst - 16 s_j, L + 16 s_j
+	uint8_t ring[RING];  // filled by LDS-DMA, STG-byte slots
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// 16 bytes from global memory at a, never reading at or past lim.
+// Diagnostic build only (-DLZ4ADA_SP_STAMPS): cycles per phase and event
+// counts, summed over waves (no draining: a wait is timed as it stands).
+enum SpPhase { SP_TOTAL, SP_DMAWAIT, SP_MWAIT, SP_MATCH, SP_GCOPY, SP_BATCHES, SP_RESTARTS, SP_SEQ,
+	           SP_SLOW, SP_NST };
+#ifdef LZ4ADA_SP_STAMPS
+__device__ unsigned long long g_sp_stamps[SP_NST];
+#define SSTAMP_DECL uint64_t sst[SP_NST] = {}; const uint64_t sst0 = __builtin_amdgcn_s_memtime()
+#define SSTAMP_BEGIN() const uint64_t _sst_t = __builtin_amdgcn_s_memtime()
+#define SSTAMP_END(ph) (sst[ph] += __builtin_amdgcn_s_memtime() - _sst_t)
+#define SCOUNT(ph, v) (sst[ph] += uint64_t(v))
+#define SSTAMP_FLUSH()                                                       \
+	do {                                                                     \
+		sst[SP_TOTAL] = __builtin_amdgcn_s_memtime() - sst0;                 \
+		if (lane_id() == 0)                                                  \
+			for (int _i = 0; _i < SP_NST; ++_i)                              \
+				atomicAdd(&g_sp_stamps[_i], (unsigned long long)sst[_i]);    \
+	} while (0)
+#else
+#define SSTAMP_DECL
+#define SSTAMP_BEGIN()
+#define SSTAMP_END(ph)
+#define SCOUNT(ph, v)
+#define SSTAMP_FLUSH()
+#endif
+
+// Wait until at most n vector-memory instructions are outstanding, n rounded
+// down to one of a few encodable counts (n is wave-uniform: scalar branches).
+__device__ __forceinline__ void vm_wait_upto(uint32_t n)
+{
+	if (n >= 63)
+		asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+	else if (n >= 48)
+		asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+	else if (n >= 32)
+		asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+	else if (n >= 24)
+		asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+	else if (n >= 16)
+		asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+	else if (n >= 12)
+		asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+	else if (n >= 8)
+		asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+	else if (n >= 4)
+		asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+	else if (n >= 2)
+		asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+	else
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void vm_wait_all()
+{
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// 16 global bytes at a, never reading at or past lim.
 __device__ __forceinline__ u32x4 gload16(uintptr_t a, uintptr_t lim)
 {
 	u32x4 v;
@@ -68,6 +138,29 @@ __device__ __forceinline__ u32x4 gload16(uintptr_t a, uintptr_t lim)
 			t[i] = (a + i < lim) ? *reinterpret_cast<cg8*>(a + i) : 0;
 		__builtin_memcpy(&v, t, 16);
 	}
+	return v;
+}
+
+// 16 bytes at byte a of the LDS ring: three 8-byte-aligned ds_read_b64 (each
+// wrapped on its own), a one-bit dword select and four v_alignbyte.
+__device__ __forceinline__ u32x4 ring16(const uint8_t* base, uint32_t a)
+{
+	constexpr uint32_t mask = RING - 1;
+	const uint32_t a8 = a & ~7u;
+	const uint64_t q0 = *reinterpret_cast<const uint64_t*>(base + (a8 & mask));
+	const uint64_t q1 = *reinterpret_cast<const uint64_t*>(base + ((a8 + 8) & mask));
+	const uint64_t q2 = *reinterpret_cast<const uint64_t*>(base + ((a8 + 16) & mask));
+	const uint32_t w0 = uint32_t(q0), w1 = uint32_t(q0 >> 32), w2 = uint32_t(q1),
+	               w3 = uint32_t(q1 >> 32), w4 = uint32_t(q2), w5 = uint32_t(q2 >> 32);
+	const bool s1 = (a & 4u) != 0;
+	const uint32_t d0 = s1 ? w1 : w0, d1 = s1 ? w2 : w1, d2 = s1 ? w3 : w2, d3 = s1 ? w4 : w3,
+	               d4 = s1 ? w5 : w4;
+	const uint32_t sh = a & 3u;
+	u32x4 v;
+	v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+	v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+	v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+	v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
 	return v;
 }
 
@@ -127,6 +220,18 @@ __device__ __forceinline__ void gstore_n(g8* dst, u32x4 v, int32_t n)
 	}
 	if (n & 1)
 		*dst = uint8_t(lo);
+}
+
+// A literal piece of rem (>= 1) bytes at output position x: always 16 bytes
+// while they stay inside the slot -- the bytes past the run belong to its
+// match and the later sequences, all stored after this (in order, by this
+// wave), so one store instruction per piece and no partial stores.
+__device__ __forceinline__ void lit_store(g8* ob, int32_t x, u32x4 v, int32_t rem, int32_t cap)
+{
+	if (x + 16 <= cap)
+		__builtin_memcpy(ob + x, &v, 16);
+	else
+		gstore_n(ob + x, v, min(16, rem));
 }
 
 typedef unsigned __int128 u128;
@@ -232,6 +337,57 @@ __device__ __forceinline__ void run_match_wave(g8* ob, int32_t mdst, int32_t off
 	}
 }
 
+// The matches of one batch (lane j: match j of cnt; ml 0: none), every
+// byte they read already stored and completed -- except the batch's own
+// match output, which the dependency rounds order (each later round waits
+// for the earlier rounds' stores).
+__device__ __forceinline__ void run_batch_matches(g8* ob, uintptr_t olim, int32_t mdst, int32_t off,
+                                                  int32_t ml, int32_t cnt, uint32_t& nvm)
+{
+	const int32_t lane = int32_t(lane_id());
+	const bool mine = lane < cnt && ml > 0;
+	const int32_t mend = mdst + ml;
+	const int32_t src = mdst - off;
+	const int32_t dep_end = src + min(off, ml);
+	bool pend = mine;
+	// lanes [j1, c2) of the batch write bytes in [src, dep_end)
+	int32_t j1 = 0, c2 = 0;
+#pragma unroll
+	for (int stp = 32; stp >= 1; stp >>= 1) {
+		if (__shfl(lane < cnt ? mend : INT32_MAX, j1 + stp - 1) <= src)
+			j1 += stp;
+		if (__shfl(lane < cnt ? mdst : INT32_MAX, c2 + stp - 1) < dep_end)
+			c2 += stp;
+	}
+	const int32_t j2 = min(c2 - 1, lane - 1);
+	uint64_t dep = 0;
+	if (pend && j1 <= j2)
+		dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
+	for (bool first = true;; first = false) {
+		const uint64_t pending = __ballot(pend);
+		if (pending == 0)
+			break;
+		if (!first)
+			vm_wait_all();  // the previous round's stores landed
+		const bool ready = pend && (dep & pending) == 0;
+		// ready matches read no pending match's output: any order
+		if (ready && ml <= LONGM)
+			run_match(ob, mdst, off, ml, olim);
+		uint64_t lng = __ballot(ready && ml > LONGM);
+		while (lng) {
+			const int32_t j = int32_t(__builtin_ctzll(lng));
+			lng &= lng - 1;
+			run_match_wave(ob, __builtin_amdgcn_readlane(mdst, j), __builtin_amdgcn_readlane(off, j),
+			               __builtin_amdgcn_readlane(ml, j), olim);
+		}
+		if (ready)
+			pend = false;
+		nvm += 2;  // at least one load and one store instruction
+	}
+	// settle the match loads (see copy_lit): once per batch, not per sequence
+	__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_sparse(const uint8_t* __restrict__ frame,
                                                       uint64_t frame_len,
                                                       const lz4ada_block_desc* __restrict__ desc,
@@ -248,6 +404,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	g8* ob = gptr(out) + d.out_off;
 	const int32_t n = int32_t(d.in_len);
 	const int32_t cap = int32_t(d.out_cap);
+	SSTAMP_DECL;
 	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
 	const uintptr_t olim = reinterpret_cast<uintptr_t>(ob) + uintptr_t(cap);
 	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
@@ -255,17 +412,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 
 	// ---- staging: chunk c = aligned bytes [c STG, (c + 1) STG) from abase
 	// goes to ring slot c % NSLOT by LDS-DMA (global_load_lds_dwordx4, 1 KiB
-	// per instruction, no registers), DEPTH chunks ahead of the parse.  The
-	// parse issues no other memory instruction, and every batch ends with
-	// all memory settled, so "chunk c has landed" is vmcnt <= 2 (DEPTH - 1)
-	// once chunks up to c + DEPTH - 1 are issued (in-order counter; extra
-	// outstanding work only makes the wait longer, never short).
+	// per instruction, no registers).  Chunks [vlo, landed) are in the ring,
+	// [landed, issued) in flight; issued <= landed + DEPTH.
 	const uint32_t ring_lds =
 	    uint32_t(uintptr_t((__attribute__((address_space(3))) uint8_t*)(&S.ring[0])));
-	int32_t issued = 0;  // chunks [0, issued) issued
-	int32_t landed = 0;  // chunks [0, landed) known to be in LDS
+	uint32_t nvm = 0;    // vector-memory instructions issued (lower bound)
+	uint32_t dma_v = 0;  // lane s: nvm right after the DMA of the chunk in slot s was issued
+	int32_t issued = 0, landed = 0, vlo = 0;
 	const int32_t nchunks = (n + mis + STG - 1) / STG;
 	auto issue = [&](int32_t c) {
+		// the slot's previous chunk may still be read by an LDS read in flight
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 		// past the payload the chunk reads whatever follows in the frame,
 		// clamped to the frame (its bytes are never used)
 		uintptr_t g = abase + uintptr_t(c) * STG + 16u * uint32_t(lane);
@@ -285,41 +442,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			    : "s"(l), "v"(reinterpret_cast<const GLOBAL uint8_t*>(a))
 			    : "memory");
 		}
+		nvm += STG / 1024;
+		dma_v = lane == c % NSLOT ? nvm : dma_v;
+		vlo = max(vlo, c + 1 - NSLOT);
 	};
 	const int32_t maxc = nchunks;  // one chunk past the payload: 8-byte reads at its end
 	for (; issued < DEPTH && issued <= maxc; ++issued)
 		issue(issued);
-	// 8 bytes at block-relative pos (reads only move forward).  pos is
-	// wave-uniform but kept in VGPRs: the parse below runs on the VALU (four
-	// per CU) -- on the scalar unit, which the CU's eight waves share, it
-	// was SALU-bound at ~120 scalar instructions per sequence.
-	int32_t shi = 0;  // = landed * STG: bytes below it (from abase) are in LDS
+	int32_t shi = 0;  // = landed * STG: bytes below it (from abase) are in LDS (from vlo * STG on)
 	// make block-relative bytes [.., pend) readable (pend wave-uniform)
 	auto ensure = [&](int32_t pend) {
-		pend = int32_t(uni(uint32_t(pend)));  // wave-uniform: scalar control and DMA operands
+		// nothing past the payload is ever needed (the last chunk issued is
+		// the one past it)
+		pend = int32_t(uni(uint32_t(min(pend, n + 16))));
 		const int32_t need = (pend + mis - 1) / STG;  // last chunk needed
 		if (need >= issued) {
 			// a long literal run jumped past the chunks in flight: settle them
 			// and restart the stream two chunks before the one needed
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			issued = landed = max(need - 1, 0);
+			vm_wait_all();
+			SCOUNT(SP_RESTARTS, 1);
+			issued = landed = vlo = max(need - 1, 0);
 			for (int k = 0; k < DEPTH && issued <= maxc; ++k)
 				issue(issued++);
 		}
 		while (landed <= need) {
-			// chunk `landed` is the oldest in flight
-			if (issued - landed >= DEPTH)
-				asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (DEPTH - 1)) : "memory");
-			else
-				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			// chunk `landed` is the oldest in flight: everything issued after
+			// it may stay outstanding
+			SSTAMP_BEGIN();
+			vm_wait_upto(nvm - uni(uint32_t(__builtin_amdgcn_readlane(dma_v, landed % NSLOT))));
+			SSTAMP_END(SP_DMAWAIT);
 			++landed;
 			if (issued <= maxc)
-				issue(issued++);  // its slot's chunk (issued - NSLOT) is long read
+				issue(issued++);
 		}
 		shi = landed * STG;
 	};
 	// 8 bytes at block-relative pos, already readable.  pos is wave-uniform,
-	// and so is the parse on it (scalar unit).
+	// and so is the parse on it.
 	auto lds8 = [&](int32_t pos, uint32_t& lo, uint32_t& hi) {
 		const uint32_t a = uni(uint32_t(pos + mis));
 		const uint32_t r0 = a & ~3u;
@@ -359,38 +518,93 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			return x + k + 1;
 		}
 	};
+	// Literal run [lit, lit + L) -> output [dst, dst + L) (Write_Output,
+	// :790-824), now: from the ring when every byte of it is staged, else
+	// HBM -> HBM (runs longer than the staged window).  The stores are left
+	// in flight.
+	auto copy_lit = [&](int32_t lit, int32_t L, int32_t dst) {
+#ifdef LZ4ADA_SP_EXP_NOCOPY  // timing experiment (wrong output)
+		return;
+#endif
+		if (L <= 0)
+			return;
+		if (lit + mis >= vlo * STG && lit + L + mis <= shi) {
+			for (int32_t c = 0; c < L; c += 1024) {
+				const int32_t k = c + 16 * lane;
+#ifdef LZ4ADA_SP_EXP_NOSTORE  // timing experiment (wrong output): the reads only
+				if (k < L) {
+					const u32x4 v = ring16(S.ring, uint32_t(lit + mis + k));
+					asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+				}
+#else
+				if (k < L)
+					lit_store(ob, dst + k, ring16(S.ring, uint32_t(lit + mis + k)), L - k, cap);
+#endif
+				nvm += 1;
+			}
+			return;
+		}
+		SSTAMP_BEGIN();
+		for (int32_t c = 0; c < L; c += 1024 * U) {
+			u32x4 v[U];
+#pragma unroll
+			for (int u = 0; u < U; ++u) {
+				const int32_t k = c + 1024 * u + 16 * lane;
+				if (k < L)
+					v[u] = gload16(reinterpret_cast<uintptr_t>(in) + uintptr_t(lit + k), lim);
+			}
+#pragma unroll
+			for (int u = 0; u < U; ++u) {
+				const int32_t k = c + 1024 * u + 16 * lane;
+				if (k < L)
+					lit_store(ob, dst + k, v[u], L - k, cap);
+			}
+			nvm += 2;
+		}
+		// settle this rare path's loads here: left pending (lanes past the
+		// run skip the stores that wait for them), they reach the parse loop's
+		// head, and the wait pass puts a vmcnt(0) -- every DMA chunk and store
+		// in flight -- before each sequence's first LDS read
+		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+		SSTAMP_END(SP_GCOPY);
+	};
 
 	bool bad = false;
+	int32_t why = 0;   // decline reason (status detail of a DS_RETRY block: diagnostics)
 	int32_t p = 0;     // input position of the next sequence
 	int32_t o = 0;     // output position
 	int32_t nseq = 0;  // sequences so far
 	bool done = n == 0;
 	uint32_t t0 = 0, t1 = 0;  // the bytes at p (tv of them valid): the next
 	int32_t tv = 0;           // token, from the previous offset read
+	// the previous batch's matches (lane j: match j; ml 0: none), run at the
+	// end of the current batch
+	int32_t pm_dst = 0, pm_off = 1, pm_ml = 0, pm_cnt = 0;
+	uint32_t nvm_b0 = 0;  // nvm when the current batch began
+	if (!done)
+		ensure(AHEAD);
 	while (!done && !bad) {
 		// ---- parse up to NSEQ sequences (Decompress_Sequence, :737-777);
-		// sequence j of the batch lands in lane j
-		int32_t r_lit = 0, r_L = 0, r_dst = 0, r_off = 0, r_ml = 0;
-		int32_t ns = 0, pieces = 0;
-		auto record = [&](int32_t lit, int32_t L, int32_t off, int32_t ml) {
+		// each sequence's literals are copied at once, its match lands in
+		// lane j of the batch
+		int32_t m_dst = 0, m_off = 1, m_ml = 0;
+		int32_t ns = 0;
+		auto record = [&](int32_t L, int32_t off, int32_t ml) {
 			const bool mine = lane == ns;
-			r_lit = mine ? lit : r_lit;
-			r_L = mine ? L : r_L;
-			r_dst = mine ? o : r_dst;
-			r_off = mine ? off : r_off;
-			r_ml = mine ? ml : r_ml;
-			pieces += L > BIG ? 0 : (L + 15) >> 4;
+			m_dst = mine ? o + L : m_dst;
+			m_off = mine ? off : m_off;
+			m_ml = mine ? ml : m_ml;
 			o += L + ml;
 			++ns;
 		};
 		for (;;) {
-			// -- the common shape, a tight scalar loop (the CU's eight waves
-			// share one scalar unit, so instructions per sequence are the
-			// cost): the literal length's extension bytes among the token
-			// window's bytes 1..4, at most one match-length extension byte, not
-			// the last sequence, well formed, the offset within the staged
-			// bytes.  Anything else leaves it for the general code below.
-			while (ns < NSEQ && pieces <= OWN - BIG / 16 && tv >= 5 && p + mis + 1100 <= shi) {
+			// -- the common shape, a tight loop: the literal length's
+			// extension bytes among the token window's bytes 1..4, at most
+			// one match-length extension byte, not the last sequence, well
+			// formed, everything within the staged window (the run is then
+			// at most 1034 bytes, all staged).  Anything else leaves it for
+			// the general code below.
+			while (ns < NSEQ && tv >= 5 && p + mis + AHEAD <= shi) {
 				const uint32_t tk = t0 & 0xffu;
 				const uint32_t ex = uint32_t((uint64_t(t0) | (uint64_t(t1) << 32)) >> 8);  // bytes 1..4
 				const uint32_t kb = uint32_t(__builtin_ctz(~ex | 0x80000000u)) & ~7u;  // 8 x first non-0xFF
@@ -414,21 +628,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 				t0 = uint32_t(w);
 				t1 = uint32_t(w >> 32);
 				tv = 8 - used;
-				record(lit, L, off, ml);
+				copy_lit(lit, L, o);
+				record(L, off, ml);
 				p = x + used;
 			}
-			if (ns >= NSEQ || pieces > OWN - BIG / 16)
+			if (ns >= NSEQ)
 				break;
 			if (p >= n) {
 				done = true;  // the chain ended right after a match
 				break;
 			}
-			if (p + mis + 1100 > shi) {
-				ensure(p + 1100);
-				if (tv >= 5)
+			if (p + mis + AHEAD > shi) {
+				ensure(p + AHEAD);  // (the block's last AHEAD bytes: as far as it goes)
+				if (tv >= 5 && p + mis + AHEAD <= shi)
 					continue;
 			}
 			// -- one sequence, the general way (rare)
+			SCOUNT(SP_SLOW, 1);
 			rd8(p, t0, t1);
 			tv = 8;
 			const uint32_t tk = t0 & 0xffu;
@@ -437,21 +653,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			if (L == 15) {
 				lit = ext_slow(p + 1, L);
 				if (lit < 0) {
+					why = 1;
 					bad = true;
 					break;
 				}
 			}
 			const int32_t x = lit + L;
+			if (x > n || int64_t(o) + L > cap) {
+				why = 2;
+				bad = true;  // literals past the block end (D3) or the slot
+				break;
+			}
+			// the literals now, while they may still be in the ring
+			copy_lit(lit, L, o);
 			int32_t M = int32_t(tk & 15u), off = 0, ml = 0, next = n;
 			if (x >= n) {
 				// the block's last sequence: literals only (:748-764)
-				if (x > n || M != 0 || o + L > cap) {
+				if (M != 0) {
+					why = 3;
 					bad = true;
 					break;
 				}
 				done = true;
 			} else {
 				if (x + 1 >= n) {
+					why = 4;
 					bad = true;
 					break;
 				}
@@ -462,6 +688,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 				if (M == 15) {
 					next = ext_slow(x + 2, M);
 					if (next < 0) {
+						why = 5;
 						bad = true;
 						break;
 					}
@@ -470,11 +697,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 				// off 0, a reference before the block start (D2) or a slot
 				// overflow: k_decode_pc gives the exact status
 				if (off == 0 || off > o + L || int64_t(o) + L + ml > cap) {
+					why = 6;
 					bad = true;
 					break;
 				}
 			}
-			record(lit, L, off, ml);
+			record(L, off, ml);
 			p = next;
 			if (done)
 				break;
@@ -485,131 +713,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 		if (bad || ns == 0)
 			break;
 		if (nseq > p / DENSE_BYTES + 256) {
+			why = 7;
 			bad = true;  // dense data: the two-wave decoder is faster
 			break;
 		}
-
-#ifndef LZ4ADA_SP_EXP_NOLIT  // timing experiment (wrong output)
-		// ---- literals (Write_Output, :790-824): runs up to BIG bytes cut
-		// into 16-byte pieces dealt over the wave, piece t = 64 r + lane; its
-		// run from a mark at every run's first piece and a prefix maximum
-		{
-			const int32_t Lr = lane < ns ? r_L : 0;
-			const int32_t P = Lr <= BIG ? (Lr + 15) >> 4 : 0;
-			const int32_t I = wave_incl_scan(P);
-			const int32_t tot = __builtin_amdgcn_readlane(I, 63);
-			const int32_t st = I - P;
-			u32x4 rc;
-			rc.x = uint32_t(r_lit - 16 * st);
-			rc.y = uint32_t(r_dst - 16 * st);
-			rc.z = uint32_t(Lr + 16 * st);
-			rc.w = 0;
-			S.rec[lane] = rc;
-			for (int32_t z = 16 * lane; z < tot; z += 1024)
-				*reinterpret_cast<u32x4*>(&S.own[z]) = u32x4{ 0, 0, 0, 0 };
-			wave_lds_fence();
-			if (P > 0)
-				S.own[st] = uint8_t(lane);
-			wave_lds_fence();
-			int32_t carry = 0;
-			for (int32_t r0 = 0; r0 < tot; r0 += 64 * U) {
-				u32x4 v[U];
-				int32_t dd[U], ln[U];
-#pragma unroll
-				for (int u = 0; u < U; ++u) {
-					const int32_t t = r0 + 64 * u + lane;
-					const int32_t m = t < tot ? int32_t(S.own[t]) : 0;
-					const int32_t ow = max(wave_incl_max(m), carry);
-					carry = __builtin_amdgcn_readlane(ow, 63);
-					const u32x4 q = S.rec[ow];
-					ln[u] = t < tot ? min(16, int32_t(q.z) - 16 * t) : 0;
-					dd[u] = int32_t(q.y) + 16 * t;
-					if (ln[u] > 0)
-						v[u] = gload16(reinterpret_cast<uintptr_t>(in) + uintptr_t(int32_t(q.x) + 16 * t),
-						               lim);
-				}
-#pragma unroll
-				for (int u = 0; u < U; ++u)
-					if (ln[u] > 0)
-						gstore_n(ob + dd[u], v[u], ln[u]);
+		// ---- the previous batch's matches: everything they read was stored
+		// before this batch began
+		SCOUNT(SP_BATCHES, 1);
+		SCOUNT(SP_SEQ, ns);
+		if (pm_cnt > 0) {
+			{
+				SSTAMP_BEGIN();
+				vm_wait_upto(nvm - nvm_b0);
+				SSTAMP_END(SP_MWAIT);
 			}
-			// runs over BIG bytes: the whole wave, 8 KiB per step
-			uint64_t big = __ballot(lane < ns && r_L > BIG);
-			while (big) {
-				const int32_t j = int32_t(__builtin_ctzll(big));
-				big &= big - 1;
-				const int32_t Lj = __builtin_amdgcn_readlane(r_L, j);
-				const int32_t sj = __builtin_amdgcn_readlane(r_lit, j);
-				const int32_t dj = __builtin_amdgcn_readlane(r_dst, j);
-				for (int32_t c = 0; c < Lj; c += 1024 * U) {
-					u32x4 v[U];
-#pragma unroll
-					for (int u = 0; u < U; ++u) {
-						const int32_t k = c + 1024 * u + 16 * lane;
-						if (k < Lj)
-							v[u] = gload16(reinterpret_cast<uintptr_t>(in) + uintptr_t(sj + k), lim);
-					}
-#pragma unroll
-					for (int u = 0; u < U; ++u) {
-						const int32_t k = c + 1024 * u + 16 * lane;
-						if (k < Lj)
-							gstore_n(ob + dj + k, v[u], min(16, Lj - k));
-					}
-				}
-			}
+			SSTAMP_BEGIN();
+			run_batch_matches(ob, olim, pm_dst, pm_off, pm_ml, pm_cnt, nvm);
+			SSTAMP_END(SP_MATCH);
 		}
-#endif
-		// every literal (and earlier match) store has landed before a match
-		// of this batch reads the output
-		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-
-		// ---- matches in dependency rounds (Output_With_History, :845-904)
-		const int32_t mdst = r_dst + r_L;
-		const int32_t mend = mdst + r_ml;
-		const int32_t src = mdst - r_off;
-		const int32_t dep_end = src + min(r_off, r_ml);
-		bool pend = lane < ns && r_ml > 0;
-#ifdef LZ4ADA_SP_EXP_NOMATCH  // timing experiment (wrong output)
-		pend = false;
-#endif
-		// lanes [j1, c2) of the batch write bytes in [src, dep_end)
-		int32_t j1 = 0, c2 = 0;
-#pragma unroll
-		for (int stp = 32; stp >= 1; stp >>= 1) {
-			if (__shfl(lane < ns ? mend : INT32_MAX, j1 + stp - 1) <= src)
-				j1 += stp;
-			if (__shfl(lane < ns ? mdst : INT32_MAX, c2 + stp - 1) < dep_end)
-				c2 += stp;
-		}
-		const int32_t j2 = min(c2 - 1, lane - 1);
-		uint64_t dep = 0;
-		if (pend && j1 <= j2)
-			dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
-		for (;;) {
-			const uint64_t pending = __ballot(pend);
-			if (pending == 0)
-				break;
-			const bool ready = pend && (dep & pending) == 0;
-			// ready matches read no pending match's output: any order
-			if (ready && r_ml <= LONGM)
-				run_match(ob, mdst, r_off, r_ml, olim);
-			uint64_t lng = __ballot(ready && r_ml > LONGM);
-			while (lng) {
-				const int32_t j = int32_t(__builtin_ctzll(lng));
-				lng &= lng - 1;
-				run_match_wave(ob, __builtin_amdgcn_readlane(mdst, j), __builtin_amdgcn_readlane(r_off, j),
-				               __builtin_amdgcn_readlane(r_ml, j), olim);
-			}
-			if (ready)
-				pend = false;
-			__builtin_amdgcn_s_waitcnt(0x0F70);  // this round's stores landed
-		}
+		pm_dst = m_dst;
+		pm_off = m_off;
+		pm_ml = m_ml;
+		pm_cnt = ns;
+		nvm_b0 = nvm;
 	}
-	if (!bad && !done)
+	if (!bad && !done) {
+		why = 8;
 		bad = true;
+	}
+	if (!bad && pm_cnt > 0) {
+		vm_wait_all();
+		run_batch_matches(ob, olim, pm_dst, pm_off, pm_ml, pm_cnt, nvm);
+	}
+	// nothing may still be landing in this workgroup's LDS when it ends
+	vm_wait_all();
+	SSTAMP_FLUSH();
 	if (lane == 0) {
 		if (bad) {
 			status[b].code = DS_RETRY;
+			status[b].detail = why;
+			status[b].err_out_pos = uint32_t(p);
 		} else {
 			status[b].code = DS_OK;
 			status[b].aux = 0;
@@ -621,6 +764,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 }
 
 }  // namespace sparse
+
+#ifdef LZ4ADA_SP_STAMPS
+extern "C" int lz4ada_sp_stamps(unsigned long long* out, int reset)
+{
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sparse::g_sp_stamps),
+	                        sizeof(unsigned long long) * sparse::SP_NST) != hipSuccess)
+		return -1;
+	if (reset) {
+		unsigned long long z[sparse::SP_NST] = {};
+		if (hipMemcpyToSymbol(HIP_SYMBOL(sparse::g_sp_stamps), z, sizeof z) != hipSuccess)
+			return -1;
+	}
+	return sparse::SP_NST;
+}
+#endif
 
 hipError_t launch_decode_sparse(const uint8_t* d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,

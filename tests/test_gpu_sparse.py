@@ -67,6 +67,30 @@ def test_sparse_alone_exact(bmax, sizes):
     assert out == raw
 
 
+def test_sparse_long_runs_exact():
+    """Literal runs longer than the staged window (copied HBM -> HBM, the
+    staging stream restarted past them) mixed with short ones."""
+    rng = random.Random(5)
+    bmax = 4 << 20
+    blocks = []
+    for n, lo, hi in [((4 << 20) - 40000, 1500, 30000), (2 << 20, 40, 9000), (600_000, 3000, 70000)]:
+        seqs = B.sparse_seqs(rng, n, lit_lo=lo, lit_hi=hi)
+        blocks.append(B.encode(seqs, rng.randbytes(rng.randint(12, 5000))))
+    assert all(len(r) <= bmax for _, r in blocks)
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, block_cksum=True)
+    st0, want, _, msg = O.decode_stream(frame)
+    assert st0 == O.OK and want == raw, msg
+    info, st1, _ = run_variant(frame, lz4ada.DECODE_IDX_ALONE)
+    sp = [i for i in range(len(blocks)) if st1[i].code == lz4ada.DS_SPARSE]
+    assert len(sp) >= 2, [s.code for s in st1[:len(blocks)]]  # pass 1 hands them over
+    info, st, outs = run_variant(frame, lz4ada.DECODE_IDX_SPARSE)
+    for i in sp:
+        assert st[i].code == 0, (i, st[i].code, st[i].detail, st[i].err_out_pos)
+        assert outs[i] == blocks[i][1], i
+    out, _ = lz4ada.decode_frame(frame)
+    assert out == raw
+
+
 def test_literal_class_taken_by_sparse():
     """The bench's literal class (4 MiB blocks) is pass 1's sparse case and
     k_decode_sparse's whole job."""
