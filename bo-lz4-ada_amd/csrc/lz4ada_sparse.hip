@@ -409,6 +409,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	const uintptr_t olim = reinterpret_cast<uintptr_t>(ob) + uintptr_t(cap);
 	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
 	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
+	// A lane whose 16-byte DMA piece would cross the frame's end loads an
+	// earlier piece instead (below), so ring bytes from the last 16-byte
+	// boundary before the frame's end on are not the stream's: block-relative
+	// bytes at or past rbad are read from HBM.
+	const int32_t rbad =
+	    int32_t(min(uintptr_t(lim - abase) & ~uintptr_t(15), uintptr_t(INT32_MAX / 2))) - mis;
 
 	// ---- staging: chunk c = aligned bytes [c STG, (c + 1) STG) from abase
 	// goes to ring slot c % NSLOT by LDS-DMA (global_load_lds_dwordx4, 1 KiB
@@ -491,6 +497,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	};
 	auto rd8 = [&](int32_t pos, uint32_t& lo, uint32_t& hi) {
 		pos = int32_t(uni(uint32_t(pos)));
+		if (pos + 8 > rbad) {
+			// the stream's last bytes: from HBM, never at or past the frame's end
+			uint64_t v = 0;
+			for (int k = 0; k < 8; ++k)
+				if (reinterpret_cast<uintptr_t>(in) + uintptr_t(pos + k) < lim)
+					v |= uint64_t(in[pos + k]) << (8 * k);
+			__builtin_amdgcn_s_waitcnt(0x0F70);  // settled here (see copy_lit)
+			lo = uni(uint32_t(v));
+			hi = uni(uint32_t(v >> 32));
+			return;
+		}
 		if (pos + mis + 8 > shi)
 			ensure(pos + 8);
 		lds8(pos, lo, hi);
@@ -528,7 +545,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #endif
 		if (L <= 0)
 			return;
-		if (lit + mis >= vlo * STG && lit + L + mis <= shi) {
+		if (lit + mis >= vlo * STG && lit + L + mis <= shi && lit + L <= rbad) {
 			for (int32_t c = 0; c < L; c += 1024) {
 				const int32_t k = c + 16 * lane;
 #ifdef LZ4ADA_SP_EXP_NOSTORE  // timing experiment (wrong output): the reads only
@@ -575,8 +592,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	int32_t o = 0;     // output position
 	int32_t nseq = 0;  // sequences so far
 	bool done = n == 0;
-	uint32_t t0 = 0, t1 = 0;  // the bytes at p (tv of them valid): the next
-	int32_t tv = 0;           // token, from the previous offset read
+	u32x4 win = {0u, 0u, 0u, 0u};  // the bytes at p (tv of them valid): the next
+	int32_t tv = 0;                // token, from the previous offset read
 	// the previous batch's matches (lane j: match j; ml 0: none), run at the
 	// end of the current batch
 	int32_t pm_dst = 0, pm_off = 1, pm_ml = 0, pm_cnt = 0;
@@ -598,39 +615,100 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			++ns;
 		};
 		for (;;) {
-			// -- the common shape, a tight loop: the literal length's
-			// extension bytes among the token window's bytes 1..4, at most
-			// one match-length extension byte, not the last sequence, well
-			// formed, everything within the staged window (the run is then
-			// at most 1034 bytes, all staged).  Anything else leaves it for
-			// the general code below.
-			while (ns < NSEQ && tv >= 5 && p + mis + AHEAD <= shi) {
-				const uint32_t tk = t0 & 0xffu;
-				const uint32_t ex = uint32_t((uint64_t(t0) | (uint64_t(t1) << 32)) >> 8);  // bytes 1..4
-				const uint32_t kb = uint32_t(__builtin_ctz(~ex | 0x80000000u)) & ~7u;  // 8 x first non-0xFF
-				const bool isx = tk >= 0xf0u;
-				const int32_t L = isx ? int32_t(15 + 255 * (kb >> 3) + ((ex >> kb) & 0xffu)) : int32_t(tk >> 4);
-				const int32_t lit = p + 1 + (isx ? int32_t(kb >> 3) + 1 : 0);
-				const int32_t x = lit + L;
-				if ((isx && (~ex) == 0u) || x + 1 >= n)
-					break;
-				uint32_t w0, w1;
-				lds8(x, w0, w1);  // offset, match-length byte, the next token
-				const int32_t off = int32_t(w0 & 0xffffu);
-				const int32_t M = int32_t(tk & 15u);
-				const uint32_t e = (w0 >> 16) & 0xffu;
-				const bool x2 = M == 15;
-				const int32_t ml = M + 4 + (x2 ? int32_t(e) : 0);
-				if ((x2 && e == 255u) || off == 0 || off > o + L || o + L + ml > cap)
-					break;
-				const int32_t used = x2 ? 3 : 2;  // the next token is in w
-				const uint64_t w = (uint64_t(w0) | (uint64_t(w1) << 32)) >> (8 * used);
-				t0 = uint32_t(w);
-				t1 = uint32_t(w >> 32);
-				tv = 8 - used;
-				copy_lit(lit, L, o);
-				record(L, off, ml);
-				p = x + used;
+			// -- the common shape: the literal length's extension among the
+			// 16-byte window's bytes, at most one match-length extension byte,
+			// not the last sequence, well formed, run and offset staged (runs
+			// up to 3074 bytes: 99.9% of the literal class, against 91% for
+			// the 8-byte window before); the literals stored branch-free.
+			// Anything else leaves the sequence to the general code below.
+			// The parse is wave-uniform and runs on the scalar unit; on the
+			// VALU (LZ4ADA_SP_VALU: the state laundered into VGPRs, every lane
+			// computing the same values) the decoder alone is faster (6.8 vs
+			// 7.4 ms) but the step with the block checksums beside it slower
+			// (9.4 vs 8.7 ms): their XXH32 chains wait on the same VALUs.
+			{
+				int32_t vp = p, vo = o, vns = ns, vtv = tv;
+				u32x4 w = win;
+				// (LZ4ADA_SP_VALU: kept in VGPRs, opaque to the uniformity
+				// analysis, so everything derived from them stays on the VALU)
+#ifdef LZ4ADA_SP_VALU
+				asm volatile("" : "+v"(vp), "+v"(vo), "+v"(vns), "+v"(vtv), "+v"(w.x), "+v"(w.y), "+v"(w.z),
+				             "+v"(w.w));
+#endif
+				for (;;) {
+					const uint32_t tk = w.x & 0xffu;
+					const int32_t L4 = int32_t(tk >> 4), M4 = int32_t(tk & 15u);
+					// first byte != 0xFF among the window's bytes 1..15 (i = 16:
+					// none): per dword the lowest set bit of its complement
+					// (v_ffbl; 128 when none), the minimum over the four
+					auto ff = [](uint32_t m) -> uint32_t { return m ? uint32_t(__builtin_ctz(m)) : 128u; };
+					const uint32_t fb = min(min(ff(~w.x & 0xFFFFFF00u), 32u + ff(~w.y)),
+					                        min(64u + ff(~w.z), 96u + ff(~w.w)));
+					const int32_t i = int32_t(min(fb >> 3, 16u));
+					const uint32_t wd = (i & 8) ? ((i & 4) ? w.w : w.z) : ((i & 4) ? w.y : w.x);
+					const uint32_t bi = (wd >> (8 * (i & 3))) & 0xffu;
+					const bool isx = L4 == 15;
+					const int32_t L = isx ? 15 + 255 * (i - 1) + int32_t(bi) : L4;
+					const int32_t lit = vp + 1 + (isx ? i : 0);
+					const int32_t x = lit + L;
+					// staged through x + 16 (a chunk at a time, every few sequences)
+					// (only for a length read within the window: x stays within 3.1 KiB of
+					// vp, so the chunks ensure() recycles are all behind vp)
+					if (uni(uint32_t(x + mis + 16 > shi && (!isx || i < vtv))))
+						ensure(int32_t(uni(uint32_t(x + 16))));
+					const u32x4 y = ring16(S.ring, uint32_t(x + mis));  // offset, ML byte, next token...
+					const int32_t off = int32_t(y.x & 0xffffu);
+					const uint32_t e = (y.x >> 16) & 0xffu;
+					const bool x2 = M4 == 15;
+					const int32_t ml = M4 + 4 + (x2 ? int32_t(e) : 0);
+					const int32_t used = x2 ? 3 : 2;
+					const bool ok = vns < NSEQ && vtv >= 1 && (!isx || i < vtv) && x + 1 < n &&
+					                x + mis + 16 <= shi && x + 16 <= rbad && lit + mis >= vlo * STG &&
+					                !(x2 && e == 255u) &&
+					                off != 0 && off <= vo + L && vo + L + ml + 16 <= cap;
+					if (!uni(uint32_t(ok)))
+						break;
+					// the literals: lane j stores piece j (16 bytes; pieces past the
+					// run repeat the last one, so no lane is masked off; the bytes a
+					// piece spills past the run are rewritten later)
+					const int32_t last = max((L - 1) >> 4, 0);
+#ifndef LZ4ADA_SP_EXP_NOCOPY  // timing experiment (wrong output)
+					{
+						const int32_t j = min(lane, last);
+						const u32x4 v = ring16(S.ring, uint32_t(lit + mis + 16 * j));
+						__builtin_memcpy(ob + vo + 16 * j, &v, 16);
+					}
+					if (uni(uint32_t(L > 1024))) {
+#pragma unroll
+						for (int r = 1; r < 4; ++r) {
+							const int32_t j = min(64 * r + lane, last);
+							const u32x4 v = ring16(S.ring, uint32_t(lit + mis + 16 * j));
+							__builtin_memcpy(ob + vo + 16 * j, &v, 16);
+						}
+						nvm += 3;
+					}
+					nvm += 1;
+#endif
+					const bool mine = lane == vns;
+					m_dst = mine ? vo + L : m_dst;
+					m_off = mine ? off : m_off;
+					m_ml = mine ? ml : m_ml;
+					vo += L + ml;
+					vns += 1;
+					vp = x + used;
+					// the next window: y from byte `used` on
+					const uint32_t sh = uint32_t(used);
+					w.x = __builtin_amdgcn_alignbyte(y.y, y.x, sh);
+					w.y = __builtin_amdgcn_alignbyte(y.z, y.y, sh);
+					w.z = __builtin_amdgcn_alignbyte(y.w, y.z, sh);
+					w.w = y.w >> (8 * sh);
+					vtv = 16 - used;
+				}
+				p = int32_t(uni(uint32_t(vp)));
+				o = int32_t(uni(uint32_t(vo)));
+				ns = int32_t(uni(uint32_t(vns)));
+				tv = int32_t(uni(uint32_t(vtv)));
+				win = w;
 			}
 			if (ns >= NSEQ)
 				break;
@@ -638,15 +716,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 				done = true;  // the chain ended right after a match
 				break;
 			}
-			if (p + mis + AHEAD > shi) {
-				ensure(p + AHEAD);  // (the block's last AHEAD bytes: as far as it goes)
-				if (tv >= 5 && p + mis + AHEAD <= shi)
-					continue;
-			}
 			// -- one sequence, the general way (rare)
 			SCOUNT(SP_SLOW, 1);
+			uint32_t t0, t1;
 			rd8(p, t0, t1);
-			tv = 8;
 			const uint32_t tk = t0 & 0xffu;
 			int32_t L = int32_t(tk >> 4);
 			int32_t lit = p + 1;
@@ -706,8 +779,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			p = next;
 			if (done)
 				break;
-			rd8(p, t0, t1);  // the next token's window
-			tv = 8;
+			// the next token's window
+			if (p + mis + 16 > shi)
+				ensure(p + 16);
+			win = ring16(S.ring, uint32_t(p + mis));
+			tv = max(min(rbad - p, 16), 0);  // (0: the general path takes the rest)
 		}
 		nseq += ns;
 		if (bad || ns == 0)
