@@ -57,6 +57,13 @@ constexpr int32_t LEAD_SEQ = LZ4ADA_LEAD_SEQ;
 #define LZ4ADA_LEAD_MAX 1024
 #endif
 constexpr int32_t LEAD_IN0 = 256, LEAD_MIN = 256, LEAD_MAX = LZ4ADA_LEAD_MAX;
+// Blocks with more than RLE_RATIO output bytes (slot capacity) per input
+// byte are declined as sparse before any walk: few sequences with huge
+// matches (runs), whose length extensions of hundreds of 255-bytes make the
+// speculative walks crawl a lane per fixed-point iteration (53 per chunk,
+// ~125k cycles each) -- k_decode_sparse's case (it declines dense data
+// itself, so no result changes).
+constexpr uint64_t RLE_RATIO = 64;
 
 // vmcnt(0) through the builtin, so the compiler's wait pass sees it (an asm
 // wait leaves the loads pending in its model: later register reuse on any
@@ -461,6 +468,11 @@ __device__ __forceinline__ void index_block(IdxLds& X, const uint8_t* __restrict
 			status[b].code = DS_OK;
 		return;
 	}
+	if (uint64_t(d.in_len) * RLE_RATIO < uint64_t(d.out_cap)) {
+		if (lane == 0)
+			status[b].code = DS_SPARSE;
+		return;
+	}
 	cg8* in = gptr(frame) + d.in_off;
 	const int32_t n = int32_t(d.in_len);
 	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
@@ -572,6 +584,7 @@ __device__ __forceinline__ void index_block(IdxLds& X, const uint8_t* __restrict
 		// lane's records are those of its last walk: to HBM, coalesced
 		if (s < n && err)
 			bad = true;
+
 		bad = __any(bad);
 		wave_lds_fence();
 		int32_t starts = 0;  // sequence starts in this chunk (sizes the next lead-in)

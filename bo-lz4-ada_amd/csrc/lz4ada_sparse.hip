@@ -519,6 +519,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 		for (;;) {
 			if (x >= n || len > cap)
 				return -1;
+			if (x + 64 <= rbad) {
+				// 64 bytes a step, one per lane: a ballot of the bytes that are
+				// not 255 (RLE blocks carry runs of hundreds of them)
+				if (x + mis + 64 > shi)
+					ensure(x + 64);
+				const uint32_t bv = S.ring[uint32_t(x + mis + lane) & (RING - 1)];
+				const uint64_t nf = __ballot(bv != 0xFFu);
+				if (nf == 0) {
+					len += 255 * 64;
+					x += 64;
+					continue;
+				}
+				const int32_t k = int32_t(__builtin_ctzll(nf));
+				if (x + k >= n)
+					return -1;
+				len += 255 * k + int32_t(__builtin_amdgcn_readlane(bv, k));
+				return x + k + 1;
+			}
 			uint32_t lo, hi;
 			rd8(x, lo, hi);
 			const uint64_t w = uint64_t(lo) | (uint64_t(hi) << 32);

@@ -104,6 +104,23 @@ def test_literal_class_taken_by_sparse():
         assert st[i].code == 0 and outs[i] == r, i
 
 
+@pytest.mark.parametrize("bmax", [4 << 20, 64 << 10])
+def test_rle_class_taken_by_sparse(bmax):
+    """RLE blocks (more than 64 output bytes per input byte; runs of 255-bytes
+    in the match-length extensions, on which pass 1's speculative walks would
+    crawl) are handed to the scalar-parse decoder before any walk; its
+    whole-wave pattern fills write them."""
+    blocks = [lz4ada.gen_block(lz4ada.GEN_RLE, 0x4C5A3441 + i, bmax) for i in range(3)]
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, block_cksum=True)
+    info, st, outs = run_variant(frame, lz4ada.DECODE_IDX_ALONE)
+    assert all(s.code == lz4ada.DS_SPARSE for s in st[:3]), [s.code for s in st[:3]]
+    info, st, outs = run_variant(frame, lz4ada.DECODE_IDX_SPARSE)
+    for i, (c, r) in enumerate(blocks):
+        if st[i].code == 0:
+            assert outs[i] == r, i
+    assert lz4ada.decode_frame(frame)[0] == raw
+
+
 def _with_fault(kind):
     rng = random.Random(23)
     seqs = B.sparse_seqs(rng, 1 << 20)
