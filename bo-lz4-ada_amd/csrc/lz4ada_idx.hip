@@ -63,7 +63,10 @@ constexpr int32_t LEAD_IN0 = 256, LEAD_MIN = 256, LEAD_MAX = LZ4ADA_LEAD_MAX;
 // speculative walks crawl a lane per fixed-point iteration (53 per chunk,
 // ~125k cycles each) -- k_decode_sparse's case (it declines dense data
 // itself, so no result changes).
+// (RLE_MIN_IN: the slot capacity overstates a short block's output, e.g. a
+// frame's last block, and small blocks cost pass 1 little either way.)
 constexpr uint64_t RLE_RATIO = 64;
+constexpr uint32_t RLE_MIN_IN = 4096;
 
 // vmcnt(0) through the builtin, so the compiler's wait pass sees it (an asm
 // wait leaves the loads pending in its model: later register reuse on any
@@ -468,7 +471,7 @@ __device__ __forceinline__ void index_block(IdxLds& X, const uint8_t* __restrict
 			status[b].code = DS_OK;
 		return;
 	}
-	if (uint64_t(d.in_len) * RLE_RATIO < uint64_t(d.out_cap)) {
+	if (d.in_len >= RLE_MIN_IN && uint64_t(d.in_len) * RLE_RATIO < uint64_t(d.out_cap)) {
 		if (lane == 0)
 			status[b].code = DS_SPARSE;
 		return;
