@@ -38,6 +38,9 @@
 namespace lz4ada {
 namespace idx {
 
+#ifndef LZ4ADA_STORED_NT
+#define LZ4ADA_STORED_NT 0
+#endif
 constexpr int SEG = 256;            // pass-1 segment per lane
 constexpr int CHUNK = 64 * SEG;     // pass-1 staged chunk (16 KiB)
 constexpr int SUB = 32;             // pass-2 sub-segment per lane
@@ -701,7 +704,10 @@ __device__ __forceinline__ void wave_match(g8* ob, uintptr_t olim, int32_t dst, 
 	}
 }
 
-// Whole-wave copy of one literal run from the compressed input.
+// Whole-wave copy of one literal run from the compressed input.  NT
+// (stored blocks, experiment LZ4ADA_STORED_NT): 1 = nontemporal stores,
+// 2 = nontemporal loads too.
+template <int NT = 0>
 __device__ __forceinline__ void wave_literal(g8* ob, int32_t dst, const Src& S, int32_t src,
                                              int32_t len)
 {
@@ -714,13 +720,18 @@ __device__ __forceinline__ void wave_literal(g8* ob, int32_t dst, const Src& S, 
 #pragma unroll
 		for (int u = 0; u < U; ++u) {
 			const int32_t k = c + 1024 * u + 16 * lane;
-			if (k < len)
-				v[u] = gload16(reinterpret_cast<uintptr_t>(S.in) + uintptr_t(src + k), S.lim);
+			const uintptr_t a = reinterpret_cast<uintptr_t>(S.in) + uintptr_t(src + k);
+			if (NT >= 2 && k + 16 <= len && a + 16 <= S.lim)
+				v[u] = __builtin_nontemporal_load(reinterpret_cast<const GLOBAL u32x4*>(a));
+			else if (k < len)
+				v[u] = gload16(a, S.lim);
 		}
 #pragma unroll
 		for (int u = 0; u < U; ++u) {
 			const int32_t k = c + 1024 * u + 16 * lane;
-			if (k < len)
+			if (NT >= 1 && k + 16 <= len)
+				__builtin_nontemporal_store(v[u], reinterpret_cast<GLOBAL u32x4*>(ob + dst + k));
+			else if (k < len)
 				gstore_n(ob + dst + k, v[u], min(16, len - k));
 		}
 	}
@@ -1291,7 +1302,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			Src S0;
 			S0.in = in;
 			S0.lim = lim;
-			wave_literal(ob, 0, S0, 0, n);
+			wave_literal<LZ4ADA_STORED_NT>(ob, 0, S0, 0, n);
 		}
 		if (lane == 0) {
 			status[b].code = code;
