@@ -74,6 +74,8 @@ def parse_args(argv=None):
                     help="skip the configs[4] row (1 GiB linked frame, 256 KiB blocks)")
     ap.add_argument("--no-64k", action="store_true",
                     help="skip the configs[1] row (1 GiB frame, 64 KiB blocks)")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the c3_one_gpu row (configs[3]'s 32 GiB frame on one GPU)")
     ap.add_argument("--launch-check", action="store_true",
                     help="test hook: start the ranks, check the process group (gloo, no GPU), "
                          "print one JSON line")
@@ -99,6 +101,23 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def kernel_src_hash() -> str:
+    """sha256 (16 hex digits) of the device-code sources and build flags
+    (bo-lz4-ada_amd/csrc/*.hip, *.h, Makefile): profiles/pmc_decode.json
+    records the hash it was measured with, and bench.py reports its traffic
+    only when the hash still matches (a kernel change voids the figure)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "bo-lz4-ada_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
+                    [os.path.join(csrc, "Makefile")]):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 # ------------------------------------------------------------- synthetic data
 
 def make_unique_blocks(lz4ada, lz4frame, xxhash, kind, n_unique, block_max, block_cksum=True):
@@ -120,32 +139,42 @@ def make_unique_blocks(lz4ada, lz4frame, xxhash, kind, n_unique, block_max, bloc
 
 
 def assemble_shard(lz4ada, torch, recs, first_block, nblocks, block_max, dev):
-    """This rank's shard of the tiled frame, assembled in host memory and
-    copied to the GPU in one transfer (no per-block device copies)."""
+    """This rank's shard of the tiled frame: the unique blocks cycle with
+    period len(recs) from `first_block`, so one period (rotated to start
+    there) is assembled in host memory, copied to the GPU once and tiled on
+    the device -- a 16 GiB shard costs one ~130 MiB host assembly."""
     import numpy as np
     n_unique = len(recs)
-    order = [(first_block + i) % n_unique for i in range(nblocks)]
+    period = min(n_unique, nblocks)
+    order = [(first_block + i) % n_unique for i in range(period)]
     lens = [len(recs[u][0]) for u in order]
-    offs = [0] * nblocks
-    pos = 0
-    for i, ln in enumerate(lens):
-        offs[i] = pos
+    poffs, pos = [], 0
+    for ln in lens:
+        poffs.append(pos)
         pos += ln
-    frame_len = pos + 64
-    host = np.empty(frame_len, dtype=np.uint8)
-    host[pos:] = 0
-    arrs = [np.frombuffer(r[0], dtype=np.uint8) for r in recs]
+    tile_len = pos
+    host = np.empty(tile_len, dtype=np.uint8)
     for i, u in enumerate(order):
-        host[offs[i]:offs[i] + lens[i]] = arrs[u]
-    d_frame = torch.from_numpy(host).to(dev)
-    del host
+        host[poffs[i]:poffs[i] + lens[i]] = np.frombuffer(recs[u][0], dtype=np.uint8)
+    tile = torch.from_numpy(host).to(dev)
+    reps, rest = divmod(nblocks, period)
+    rest_len = poffs[rest] if rest else 0
+    parts = [tile.repeat(reps)] if reps else []
+    if rest:
+        parts.append(tile[:rest_len])
+    parts.append(torch.zeros(64, dtype=torch.uint8, device=dev))
+    d_frame = torch.cat(parts) if len(parts) > 1 else parts[0]
+    del tile, parts, host
+    frame_len = reps * tile_len + rest_len + 64
     descs = (lz4ada.BlockDesc * nblocks)()
     exp_hash = []
     comp_bytes = raw_bytes = 0
-    for i, u in enumerate(order):
+    for i in range(nblocks):
+        q, j = divmod(i, period)
+        u = order[j]
         rec, clen, rlen, h = recs[u][:4]
         d = descs[i]
-        d.in_off = offs[i] + 4
+        d.in_off = q * tile_len + poffs[j] + 4
         d.in_len = clen
         stored = (int.from_bytes(rec[:4], "little") >> 31) & 1
         has_ck = len(rec) == clen + 8
@@ -157,7 +186,8 @@ def assemble_shard(lz4ada, torch, recs, first_block, nblocks, block_max, dev):
         comp_bytes += clen
         raw_bytes += rlen
     d_desc = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
-    torch.cuda.synchronize()
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize()
     return d_frame, frame_len, d_desc, exp_hash, comp_bytes, raw_bytes, descs
 
 
@@ -307,6 +337,42 @@ def bench_class(M, dev, sh, stream, cls, nb, bmax, block_cksum=True, unique=16):
            "golden": "per-block XXH32 of the output vs the generator"}
     del fr, de, d_out
     return row
+
+
+def bench_c3_one_gpu(M, dev, sh, stream, recs, bmax, nblocks=C3_BLOCKS, reps=3):
+    """configs[3]'s whole frame (8192 x 4 MiB blocks, 32 GiB decoded) on ONE
+    GPU -- the same-frame N=1 point of the 1->8 curve (N>1 lines split this
+    frame over the ranks).  48 GiB of frame + output fit one MI355X's HBM."""
+    lz4ada, lz4frame, xxhash, torch = M
+    d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = assemble_shard(
+        lz4ada, torch, recs, 0, nblocks, bmax, dev)
+    d_out = torch.empty(nblocks * bmax, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nblocks * 32, dtype=torch.uint8, device=dev)
+    d_hash = torch.zeros(nblocks, dtype=torch.int32, device=dev)
+    fp, dp, op, sp = d_frame.data_ptr(), d_desc.data_ptr(), d_out.data_ptr(), d_st.data_ptr()
+    lz4ada.decode_blocks_device(fp, frame_len, dp, nblocks, op, sp, sh)
+    torch.cuda.synchronize()
+    golden_check(lz4ada, torch, d_st, descs, nblocks, op, dp, sp, d_hash, exp_hash, sh, "c3 one GPU")
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        lz4ada.decode_blocks_device(fp, frame_len, dp, nblocks, op, sp, sh)
+        b.record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    ms = sum(a.elapsed_time(b) for a, b in ev) / reps
+    del d_frame, d_out, d_desc, d_st, d_hash
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[3] frame on one GPU: {nblocks} x 4 MiB independent blocks = "
+                        f"{raw >> 30} GiB decoded, FLG 0x70 (B.Indep|B.Checksum)",
+            "blocks": nblocks, "kernel_ms": round(ms, 3), "wall_ms": round(wall * 1e3, 3),
+            "value": round(raw / (wall) / MiB, 1), "unit": "MiB/s",
+            "frac": round((comp + raw) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "compressed_bytes": comp, "decoded_bytes": raw,
+            "note": "same frame as the --gpus N>1 lines (strong scaling): N=1 point of the curve",
+            "golden": "per-block XXH32 of the output vs the generator"}
 
 
 def bench_linked(M, dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, chain=64):
@@ -575,12 +641,16 @@ def main():
     alg_bytes = comp_bytes + raw_bytes  # compressed read once + output written once
     achieved = alg_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None
+    traffic_src = None
     if os.path.exists(args.pmc):
         with open(args.pmc) as fh:
             pmc = json.load(fh)
+        # only a figure measured on this workload with these kernel sources
         if (pmc.get("config") == {"kind": args.kind, "blocks": nb, "block_max": bmax}
-                and pmc.get("kernel") == dec_kernel):
+                and pmc.get("kernel") == dec_kernel
+                and pmc.get("kernel_src_sha16") == kernel_src_hash()):
             traffic = pmc.get("hbm_bytes_per_launch")
+            traffic_src = pmc.get("source")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "kernel": dec_kernel, "kernel_ms": round(dec_ms, 3),
@@ -589,6 +659,7 @@ def main():
                               "wave) with k_xxh32_rows (block checksums) overlapped on the side "
                               "stream",
             "alg_bytes_per_launch": alg_bytes,
+            "traffic_source": traffic_src, "kernel_src_sha16": kernel_src_hash(),
             "alone_ms": alone}
 
     if world > 1:
@@ -614,6 +685,14 @@ def main():
     }
     if world > 1:
         result["rccl_ranks"] = dist.get_world_size()
+        # every rank's block count and decode time (HIP events on its stream)
+        mine = torch.tensor([float(nb), dec_ms, elapsed / args.steps * 1e3], dtype=torch.float64,
+                            device=dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        result["per_rank"] = [{"rank": r, "blocks_per_gpu": int(t[0].item()),
+                               "kernel_ms": round(float(t[1].item()), 3)}
+                              for r, t in enumerate(allr)]
 
     extra = world == 1 and rank == 0
     # ---- configs[2] e2e: + frame-wide content XXH32 (one serial chain), run
@@ -633,6 +712,14 @@ def main():
             "note": "frame-wide XXH32 is one serial 4-lane chain (SURVEY H2): decoded bytes "
                     "stream to the host in 32 MiB chunks, each hashed by one host core while "
                     "the next is in flight (one GPU wave runs the chain at ~1.1 GB/s)"}
+
+    # ---- configs[3]'s frame on this one GPU (the curve's same-frame N=1 point)
+    if extra and not args.no_c3:
+        del d_out, d_frame
+        torch.cuda.empty_cache()
+        log("[bench] c3_one_gpu (8192 x 4 MiB on one GPU) ...")
+        result["c3_one_gpu"] = bench_c3_one_gpu(M, dev, sh, stream, recs, bmax)
+        d_out = None
 
     # ---- other content classes through the product call, same layout
     if extra:

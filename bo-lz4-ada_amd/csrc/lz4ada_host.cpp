@@ -775,15 +775,35 @@ struct lz4ada_decompressor {
 	// k_serial_block, which redoes it from the same state on an untouched
 	// mirror.  launch_fast_block enqueues the decode and returns the block's
 	// Output_Pos (-1: not tried); finish_fast_block waits for it.
+	// The output room a decoder slot needs for one block: what the Buffer
+	// leaves, but no more than the frame's block maximum (BD for modern
+	// frames, 8 MiB for legacy ones, lz4ada.adb:65-77, 225-239) or 255 bytes
+	// per payload byte.  A block that would decode to more is the exact
+	// path's (the reference bounds it by the Buffer alone, D5) -- so a large
+	// caller Buffer never sizes the device scratch.
+	int64_t block_room(int64_t buflen_left, int64_t raw_len, bool compressed) const
+	{
+		int64_t cap = std::min<int64_t>(buflen_left, INT32_MAX);
+		if (compressed)
+			cap = std::min<int64_t>(cap, 255 * std::max<int64_t>(raw_len, 1) + 16);
+		else
+			cap = std::min<int64_t>(cap, raw_len);
+		if (m.is_format == F_MODERN)
+			cap = std::min<int64_t>(cap, int64_t(1) << (8 + 2 * ((m.bd & 0x70u) >> 4)));
+		else if (m.is_format == F_LEGACY)
+			cap = std::min<int64_t>(cap, int64_t(8) << 20);
+		return cap;
+	}
+
 	int64_t launch_fast_block(int64_t raw_len, int64_t blen, int64_t buflen)
 	{
 		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
 		if (linked || getenv("LZ4ADA_FACADE_EXACT"))
 			return -1;
 		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;  // :678-680
-		const int64_t cap = std::min<int64_t>(buflen - start, INT32_MAX);
-		if (cap <= 0 || raw_len > INT32_MAX)
+		if (buflen - start <= 0 || raw_len > INT32_MAX)
 			return -1;
+		const int64_t cap = std::max<int64_t>(block_room(buflen - start, raw_len, m.is_compressed), 1);
 		d_scr.reserve(size_t(cap));
 		lz4ada_block_desc d{};
 		d.in_off = 0;
@@ -792,7 +812,7 @@ struct lz4ada_decompressor {
 		d.out_off = 0;
 		d.out_cap = uint32_t(cap);
 		const int fv = facade_variant();
-		if (fv < 0 && m.is_compressed && raw_len >= LONE_MIN) {
+		if (fv < 0 && m.is_compressed && raw_len >= LONE_MIN && cap <= (int64_t(1) << 30)) {
 			const int64_t sb = lone_scratch_bytes(raw_len, cap);
 			d_lone.reserve(size_t(sb));
 			HIP_OK(launch_decode_lone(d_blk.p, raw_len, d_scr.p, cap, d_bst.p, d_lone.p, sb, stream));
@@ -839,7 +859,11 @@ struct lz4ada_decompressor {
 			return false;  // linked frame: every block needs the history (exact path)
 		const int bcl = m.block_checksum_length;
 		const int64_t avail = end - blk;
-		const uint64_t slot = (uint64_t(std::min<int64_t>(buflen, INT32_MAX)) + 255) & ~uint64_t(255);
+		// a slot holds one block: the Buffer's room, at most the block maximum
+		// (block_room with the largest payload, so every block of the batch fits)
+		const int64_t room = std::max<int64_t>(
+		        block_room(buflen, m.is_format == F_LEGACY ? (int64_t(8) << 20) : (int64_t(4) << 20), true), 1);
+		const uint64_t slot = (uint64_t(room) + 255) & ~uint64_t(255);
 		const uint64_t max_blocks = std::max<uint64_t>(1, (uint64_t(2) << 30) / slot);
 		auto add = [&](int64_t off, int64_t sz, bool stored) {
 			lz4ada_block_desc d{};
@@ -847,7 +871,7 @@ struct lz4ada_decompressor {
 			d.in_len = uint32_t(sz);
 			d.flags = (stored ? LZ4ADA_BLOCK_STORED : 0u) | (bcl ? LZ4ADA_BLOCK_HAS_CKSUM : 0u);
 			d.out_off = uint64_t(ahead.descs.size()) * slot;
-			d.out_cap = uint32_t(std::min<int64_t>(buflen, INT32_MAX));
+			d.out_cap = uint32_t(room);
 			d.cksum = bcl ? load32(blk + off + sz) : 0u;
 			ahead.descs.push_back(d);
 		};
@@ -937,15 +961,16 @@ struct lz4ada_decompressor {
 			grow_mirror(buflen);
 		const uint8_t* src = ahead.d_out.p + d.out_off;
 		if (nout > 0) {  // the mirror keeps the history for a later exact block
+			// a helper thread may still be hashing an earlier block's bytes in
+			// this Buffer range (deliver() hands large blocks to it): join it
+			// before the copy overwrites them
+			hash_wait();
 			HIP_OK(hipMemcpyAsync(d_buf.p + start, src, size_t(nout), hipMemcpyDeviceToDevice,
 			                      stream));
 			HIP_OK(hipMemcpyAsync(buf + start, src, size_t(nout), hipMemcpyDeviceToHost, stream));
 			HIP_OK(hipStreamSynchronize(stream));
 			if (m.content_checksum_length != 0)
-			{
-			hash_wait();
-			host_xxh32_update(hash_all, buf + start, size_t(nout));
-		}
+				host_xxh32_update(hash_all, buf + start, size_t(nout));
 		}
 		if (m.has_content_size)
 			m.size_remaining -= uint64_t(nout);
@@ -1901,6 +1926,7 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		d2h(st.data(), sx.p, sb, stream);
 		std::vector<int64_t> A(nb);
 		int64_t n = 0;
+		const int64_t opos0 = opos, oph0 = oph;  // this batch's start (a smaller retry rescans)
 		// the first block the exact path has to take: a block error, a
 		// checksum mismatch, or quirk D1 (a match reaching
 		// >= D1_OFF back into the history right after a block that ended at
@@ -1930,7 +1956,12 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		}
 		if (n >= (int64_t(1) << 31) - HISTORY_SIZE) {  // words hold positions + 65536 in 31 bits
 			if (nb > 1) {
+				// the smaller batch rescans from this batch's start: its own
+				// first failing block (if any) and the replayed positions
 				budget /= 2;
+				fail = -1;
+				opos = opos0;
+				oph = oph0;
 				continue;
 			}
 			return BULK_EXACT;
@@ -2078,7 +2109,12 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 				r = bulk_linked(d_frame.p, uint64_t(info.frame_len), info.block_max, descs, ls, total,
 				                lens, fail, nullptr);
 			}
-			if (r == BULK_FAIL_AT && !getenv("LZ4ADA_NO_RESUME")) {
+			// blocks before `fail` that already decode past the declared content
+			// size: the reference raises inside the first block that overruns
+			// (lz4ada.adb:830-835), which a resume at `fail` would skip -- the
+			// whole frame goes to the exact path instead
+			const bool overrun = info.has_content_size && total > info.content_size;
+			if (r == BULK_FAIL_AT && !overrun && !getenv("LZ4ADA_NO_RESUME")) {
 				// the reference outputs blocks 0 .. fail-1 and then raises in
 				// block `fail` (lz4ada.adb:672-676: each block is checked when it
 				// is reached): the exact path resumes at that block, over the

@@ -63,6 +63,56 @@ void plan(const lz4ada_block_desc* d, int64_t nb, int n, int64_t* bounds)
 		bounds[r++] = nb;
 }
 
+// A device buffer that only grows: the worker keeps one per role across
+// calls, so a repeated call allocates nothing.
+struct DevMem {
+	void* p = nullptr;
+	size_t cap = 0;
+	~DevMem()
+	{
+		if (p)
+			(void)hipFree(p);
+	}
+	hipError_t alloc(size_t n)
+	{
+		n = std::max<size_t>(n, 1);
+		if (p && n <= cap)
+			return hipSuccess;
+		reset();
+		const hipError_t e = hipMalloc(&p, n);
+		if (e != hipSuccess) {
+			p = nullptr;
+			return e;
+		}
+		cap = n;
+		return hipSuccess;
+	}
+	void reset()
+	{
+		if (p)
+			(void)hipFree(p);
+		p = nullptr;
+		cap = 0;
+	}
+	uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
+// Per-device state kept by its worker between calls (used only on the
+// worker's thread): the rank's buffers, two pinned staging chunks for the
+// H2D, a copy stream and a few decode streams, so that a group of blocks
+// decodes while the next one is still crossing PCIe.
+constexpr int NDEC = 4;
+constexpr size_t STAGE_BYTES = size_t(64) << 20;
+struct DevCache {
+	DevMem in, desc, st, out, comp, off, meta;
+	uint8_t* pinned[2] = { nullptr, nullptr };
+	hipStream_t copy = nullptr;
+	hipStream_t dec[NDEC] = {};
+	hipEvent_t landed[2] = { nullptr, nullptr };
+	hipEvent_t done[NDEC] = {};
+	int allocs = 0;  // device allocations made so far (lz4ada_multi_device_allocs)
+};
+
 // One long-lived host thread per device ordinal: its HIP stream, and the
 // per-thread side streams of the bulk decoder, live as long as the process
 // (a thread per call would leave streams behind at every call).
@@ -81,6 +131,7 @@ public:
 		return fut;
 	}
 	hipStream_t stream = nullptr;  // created by the first job, on this thread
+	DevCache cache;                // buffers and staging kept across calls
 
 private:
 	void loop()
@@ -104,13 +155,25 @@ private:
 
 std::mutex g_multi;  // one multi-GPU call at a time (the communicators are shared)
 
+// The worker of a device ordinal, created on first use.  The pool is looked
+// up from the calling thread and from the workers' own threads, so it is
+// guarded (a find racing an insert on the first multi-GPU call).
+std::mutex pool_mutex;
+std::map<int, Worker*>* pool = new std::map<int, Worker*>;  // never freed: detached threads use it
+
 Worker& worker(int dev)
 {
-	static auto* pool = new std::map<int, Worker*>;  // never freed: detached threads use it
+	std::lock_guard<std::mutex> g(pool_mutex);
 	auto it = pool->find(dev);
 	if (it == pool->end())
 		it = pool->emplace(dev, new Worker).first;
 	return *it->second;
+}
+
+bool has_worker(int dev)
+{
+	std::lock_guard<std::mutex> g(pool_mutex);
+	return pool->count(dev) != 0;
 }
 
 // RCCL communicators per device list, created once (ncclCommInitAll costs
@@ -130,23 +193,6 @@ ncclResult_t comms_for(const std::vector<int>& devs, std::vector<ncclComm_t>*& o
 	return ncclSuccess;
 }
 
-struct DevMem {
-	void* p = nullptr;
-	~DevMem()
-	{
-		if (p)
-			(void)hipFree(p);
-	}
-	hipError_t alloc(size_t n) { return hipMalloc(&p, std::max<size_t>(n, 1)); }
-	void reset()
-	{
-		if (p)
-			(void)hipFree(p);
-		p = nullptr;
-	}
-	uint8_t* u8() const { return static_cast<uint8_t*>(p); }
-};
-
 // rank status words (all-reduced with MAX: the worst one wins)
 enum : int64_t { RS_OK = 0, RS_BLOCK_ERROR = 1, RS_PRE_REF = 2, RS_DEVICE = 3 };
 
@@ -154,7 +200,6 @@ struct Rank {
 	int dev = 0;
 	int64_t lo = 0, hi = 0;
 	ncclComm_t comm = nullptr;
-	DevMem meta;  // n+1 int64 words
 	// after the all-reduce
 	std::vector<int64_t> words;
 	std::string err;  // HIP / RCCL failure on this rank
@@ -174,6 +219,14 @@ struct Rank {
 			throw std::string(what) + ": " + ncclGetErrorString(e_);                         \
 	} while (0)
 
+static void grow(DevCache& c, DevMem& m, size_t n)
+{
+	const bool fresh = !m.p || std::max<size_t>(n, 1) > m.cap;
+	TRY_HIP(m.alloc(n), "hipMalloc");
+	if (fresh)
+		++c.allocs;
+}
+
 // Phase 1 (before any collective): device, stream and the status record.
 // A rank that cannot get this far would leave the others waiting in the
 // all-reduce, so the call stops here if any rank fails.
@@ -183,19 +236,32 @@ void prepare(Rank& rk, int n)
 	TRY_HIP(hipSetDevice(rk.dev), "hipSetDevice");
 	if (!w.stream)
 		TRY_HIP(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking), "hipStreamCreate");
-	TRY_HIP(rk.meta.alloc(size_t(n + 1) * sizeof(int64_t)), "hipMalloc");
+	DevCache& c = w.cache;
+	if (!c.copy) {
+		TRY_HIP(hipStreamCreateWithFlags(&c.copy, hipStreamNonBlocking), "hipStreamCreate");
+		for (int i = 0; i < NDEC; ++i) {
+			TRY_HIP(hipStreamCreateWithFlags(&c.dec[i], hipStreamNonBlocking), "hipStreamCreate");
+			TRY_HIP(hipEventCreateWithFlags(&c.done[i], hipEventDisableTiming), "hipEventCreate");
+		}
+		for (int i = 0; i < 2; ++i) {
+			TRY_HIP(hipEventCreateWithFlags(&c.landed[i], hipEventDisableTiming), "hipEventCreate");
+			TRY_HIP(hipHostMalloc(reinterpret_cast<void**>(&c.pinned[i]), STAGE_BYTES, hipHostMallocDefault),
+			        "hipHostMalloc");
+		}
+	}
+	grow(c, c.meta, size_t(n + 1) * sizeof(int64_t));
 }
 
 // Phase 2: this rank's blocks, the all-reduce, the host copy, the gather.
-void run_rank(Rank& rk, int r, int n, const uint8_t* frame, const lz4ada_block_desc* descs,
-              int64_t block_max, uint8_t* out, int64_t out_cap, uint8_t* d_gather,
+void run_rank(Rank& rk, int r, int n, const uint8_t* frame, uint64_t frame_len,
+              const lz4ada_block_desc* descs, int64_t block_max, uint8_t* out, int64_t out_cap, uint8_t* d_gather,
               int64_t gather_cap)
 {
 	Worker& w = worker(rk.dev);
 	hipStream_t s = w.stream;
+	DevCache& c = w.cache;
 	const int64_t k = rk.hi - rk.lo;
 	int64_t status = RS_OK, total = 0;
-	DevMem d_in, d_desc, d_st, d_out, d_comp, d_off;
 	const uint8_t* d_res = nullptr;
 	try {
 		TRY_HIP(hipSetDevice(rk.dev), "hipSetDevice");
@@ -209,25 +275,60 @@ void run_rank(Rank& rk, int r, int n, const uint8_t* frame, const lz4ada_block_d
 				loc[size_t(j)].in_off = g[j].in_off - b0;
 				loc[size_t(j)].out_off = uint64_t(j) * uint64_t(block_max);
 				loc[size_t(j)].out_cap = uint32_t(block_max);
-				b1 = std::max<uint64_t>(b1, g[j].in_off + g[j].in_len);
+				b1 = std::max<uint64_t>(b1, g[j].in_off + g[j].in_len + 4);
 			}
+			b1 = std::min<uint64_t>(b1, frame_len);
 			const uint64_t out_bytes = uint64_t(k) * uint64_t(block_max);
-			TRY_HIP(d_in.alloc(b1 - b0), "hipMalloc");
-			TRY_HIP(d_desc.alloc(size_t(k) * sizeof(lz4ada_block_desc)), "hipMalloc");
-			TRY_HIP(d_st.alloc(size_t(k) * sizeof(lz4ada_block_status)), "hipMalloc");
-			TRY_HIP(d_out.alloc(out_bytes), "hipMalloc");
-			TRY_HIP(hipMemcpyAsync(d_in.p, frame + b0, b1 - b0, hipMemcpyHostToDevice, s), "H2D");
-			TRY_HIP(hipMemcpyAsync(d_desc.p, loc.data(), size_t(k) * sizeof(lz4ada_block_desc),
-			                       hipMemcpyHostToDevice, s),
+			grow(c, c.in, b1 - b0);
+			grow(c, c.desc, size_t(k) * sizeof(lz4ada_block_desc));
+			grow(c, c.st, size_t(k) * sizeof(lz4ada_block_status));
+			grow(c, c.out, out_bytes);
+			auto* d_desc = static_cast<lz4ada_block_desc*>(c.desc.p);
+			auto* d_st = static_cast<lz4ada_block_status*>(c.st.p);
+			TRY_HIP(hipMemcpyAsync(d_desc, loc.data(), size_t(k) * sizeof(lz4ada_block_desc),
+			                       hipMemcpyHostToDevice, c.copy),
 			        "H2D");
-			TRY_HIP(hipMemsetAsync(d_st.p, 0, size_t(k) * sizeof(lz4ada_block_status), s), "memset");
-			if (lz4ada_decode_blocks_device(d_in.p, b1 - b0,
-			                                static_cast<const lz4ada_block_desc*>(d_desc.p), k,
-			                                d_out.p, static_cast<lz4ada_block_status*>(d_st.p),
-			                                s) != LZ4ADA_OK)
-				throw std::string(lz4ada_thread_last_error());
+			TRY_HIP(hipMemsetAsync(d_st, 0, size_t(k) * sizeof(lz4ada_block_status), c.copy), "memset");
+			// Groups of whole blocks of at most STAGE_BYTES of input: the host
+			// copies group i into pinned chunk i & 1 while the DMA of group
+			// i - 1 runs, and group i decodes on its own stream as soon as its
+			// bytes have landed, beside the later copies.
+			int64_t j0 = 0;
+			int grp = 0;
+			while (j0 < k) {
+				int64_t j1 = j0 + 1;
+				const uint64_t g0 = loc[size_t(j0)].in_off;
+				while (j1 < k && loc[size_t(j1)].in_off + loc[size_t(j1)].in_len + 4 - g0 <= STAGE_BYTES)
+					++j1;
+				const uint64_t g1 = j1 < k ? loc[size_t(j1)].in_off - 4 : b1 - b0;  // up to the next size word
+				const int slot = grp & 1;
+				if (grp >= 2)  // the DMA that last read this chunk
+					TRY_HIP(hipEventSynchronize(c.landed[slot]), "staging");
+				for (uint64_t x = g0; x < g1;) {  // (a block over STAGE_BYTES: in pieces)
+					const uint64_t nx = std::min<uint64_t>(g1 - x, STAGE_BYTES);
+					if (x > g0)
+						TRY_HIP(hipEventSynchronize(c.landed[slot]), "staging");
+					memcpy(c.pinned[slot], frame + b0 + x, size_t(nx));
+					TRY_HIP(hipMemcpyAsync(c.in.u8() + x, c.pinned[slot], size_t(nx),
+					                       hipMemcpyHostToDevice, c.copy),
+					        "H2D");
+					TRY_HIP(hipEventRecord(c.landed[slot], c.copy), "event");
+					x += nx;
+				}
+				hipStream_t ds = c.dec[grp % NDEC];
+				TRY_HIP(hipStreamWaitEvent(ds, c.landed[slot], 0), "event wait");
+				if (lz4ada_decode_blocks_device(c.in.p, b1 - b0, d_desc + j0, j1 - j0, c.out.p,
+				                                d_st + j0, ds) != LZ4ADA_OK)
+					throw std::string(lz4ada_thread_last_error());
+				j0 = j1;
+				++grp;
+			}
+			for (int i = 0; i < NDEC && i < grp; ++i) {
+				TRY_HIP(hipEventRecord(c.done[i], c.dec[i]), "event");
+				TRY_HIP(hipStreamWaitEvent(s, c.done[i], 0), "event wait");
+			}
 			std::vector<lz4ada_block_status> st(static_cast<size_t>(k));
-			TRY_HIP(hipMemcpyAsync(st.data(), d_st.p, size_t(k) * sizeof(lz4ada_block_status),
+			TRY_HIP(hipMemcpyAsync(st.data(), d_st, size_t(k) * sizeof(lz4ada_block_status),
 			                       hipMemcpyDeviceToHost, s),
 			        "D2H");
 			TRY_HIP(hipStreamSynchronize(s), "decode");
@@ -246,19 +347,17 @@ void run_rank(Rank& rk, int r, int n, const uint8_t* frame, const lz4ada_block_d
 					contiguous = false;
 				total += b.out_len;
 			}
-			d_res = d_out.u8();
+			d_res = c.out.u8();
 			if (status == RS_OK && !contiguous) {  // a short block before the last one
-				TRY_HIP(d_comp.alloc(size_t(total)), "hipMalloc");
-				TRY_HIP(d_off.alloc(size_t(k) * sizeof(uint64_t)), "hipMalloc");
-				TRY_HIP(hipMemcpyAsync(d_off.p, dst.data(), size_t(k) * sizeof(uint64_t),
+				grow(c, c.comp, size_t(total));
+				grow(c, c.off, size_t(k) * sizeof(uint64_t));
+				TRY_HIP(hipMemcpyAsync(c.off.p, dst.data(), size_t(k) * sizeof(uint64_t),
 				                       hipMemcpyHostToDevice, s),
 				        "H2D");
-				TRY_HIP(launch_compact(d_out.u8(), static_cast<const lz4ada_block_desc*>(d_desc.p),
-				                       static_cast<const uint64_t*>(d_off.p),
-				                       static_cast<const lz4ada_block_status*>(d_st.p), uint32_t(k),
-				                       d_comp.u8(), s),
+				TRY_HIP(launch_compact(c.out.u8(), d_desc, static_cast<const uint64_t*>(c.off.p), d_st,
+				                       uint32_t(k), c.comp.u8(), s),
 				        "compact");
-				d_res = d_comp.u8();
+				d_res = c.comp.u8();
 			}
 		}
 	} catch (const std::string& e) {
@@ -271,12 +370,12 @@ void run_rank(Rank& rk, int r, int n, const uint8_t* frame, const lz4ada_block_d
 		std::vector<int64_t> words(static_cast<size_t>(n + 1), 0);
 		words[0] = status;
 		words[size_t(1 + r)] = total;
-		TRY_HIP(hipMemcpyAsync(rk.meta.p, words.data(), words.size() * sizeof(int64_t),
+		TRY_HIP(hipMemcpyAsync(c.meta.p, words.data(), words.size() * sizeof(int64_t),
 		                       hipMemcpyHostToDevice, s),
 		        "H2D");
-		TRY_NCCL(ncclAllReduce(rk.meta.p, rk.meta.p, words.size(), ncclInt64, ncclMax, rk.comm, s),
+		TRY_NCCL(ncclAllReduce(c.meta.p, c.meta.p, words.size(), ncclInt64, ncclMax, rk.comm, s),
 		         "ncclAllReduce");
-		TRY_HIP(hipMemcpyAsync(words.data(), rk.meta.p, words.size() * sizeof(int64_t),
+		TRY_HIP(hipMemcpyAsync(words.data(), c.meta.p, words.size() * sizeof(int64_t),
 		                       hipMemcpyDeviceToHost, s),
 		        "D2H");
 		TRY_HIP(hipStreamSynchronize(s), "all-reduce");
@@ -318,7 +417,6 @@ void run_rank(Rank& rk, int r, int n, const uint8_t* frame, const lz4ada_block_d
 		rk.err = e;
 		rk.landed.set_value(false);
 	}
-	rk.meta.reset();  // freed on its own device's thread
 }
 
 // The single-GPU product path on the first device: the reference's result
@@ -434,7 +532,7 @@ int decode_multi(const uint8_t* frame, int64_t len, int n, const int* devices, u
 	fut.clear();
 	for (int r = 0; r < n; ++r)
 		fut.push_back(worker(devs[size_t(r)]).run([&, r] {
-			run_rank(ranks[size_t(r)], r, n, frame, descs.data(), info.block_max, out, out_cap,
+			run_rank(ranks[size_t(r)], r, n, frame, uint64_t(info.frame_len), descs.data(), info.block_max, out, out_cap,
 			         d_gather, gather_cap);
 		}));
 	// the content checksum: one chain in frame order over the host bytes,
@@ -537,6 +635,24 @@ int lz4ada_decode_frame_multi_gather(const uint8_t* frame, int64_t len, int n_gp
 	}
 	return lz4ada::decode_multi(frame, len, n_gpus, devices, nullptr, 0,
 	                            static_cast<uint8_t*>(d_out), out_cap, out_len, frame_consumed);
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int64_t lz4ada_multi_device_allocs(int device)
+{
+	std::lock_guard<std::mutex> one(lz4ada::g_multi);
+	if (!lz4ada::has_worker(device))
+		return -1;
+	return lz4ada::worker(device).cache.allocs;
+}
+
+int lz4ada_rccl_version(void)
+{
+	int v = 0;
+	return ncclGetVersion(&v) == ncclSuccess ? v : -1;
 }
 
 }  // extern "C"

@@ -221,6 +221,8 @@ _sig = {
     "lz4ada_decode_frame_multi_gather": ([_vp, _i64, ctypes.c_int, _P(ctypes.c_int), _vp, _i64,
                                           _pi64, _pi64], ctypes.c_int),
     "lz4ada_plan_shards": ([_vp, _i64, ctypes.c_int, _pi64], ctypes.c_int),
+    "lz4ada_multi_device_allocs": ([ctypes.c_int], _i64),
+    "lz4ada_rccl_version": ([], ctypes.c_int),
     "lz4ada_lone_scratch_bytes": ([_i64, _i64], _i64),
     "lz4ada_launch_decode_lone": ([_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp], ctypes.c_int),
     "lz4ada_gen_block": ([ctypes.c_int, ctypes.c_uint64, _vp, _i64, _vp, _i64], _i64),
@@ -495,6 +497,17 @@ def plan_shards(descs, nblocks: int, n_gpus: int):
 
 
 PATH_INDEPENDENT, PATH_LINKED, PATH_EXACT, PATH_MULTI = 1, 2, 4, 8
+
+
+def multi_device_allocs(device: int) -> int:
+    """Device allocations the multi-GPU worker of `device` made so far (-1:
+    no worker yet); a repeated call of the same size adds none."""
+    return int(_lib.lz4ada_multi_device_allocs(device))
+
+
+def rccl_version() -> int:
+    """ncclGetVersion of the RCCL this process bound (22606 = 2.26.6)."""
+    return int(_lib.lz4ada_rccl_version())
 
 
 def last_path() -> int:

@@ -371,6 +371,15 @@ int lz4ada_decode_frame_multi_gather(const uint8_t *frame, int64_t len, int n_gp
  * [r, r+1) * total / n_gpus.  Host-only. */
 int lz4ada_plan_shards(const lz4ada_block_desc *descs, int64_t nblocks, int n_gpus,
                        int64_t *bounds);
+/* Device allocations the multi-GPU workers made so far for HIP ordinal
+ * `device` (each worker keeps its buffers and pinned staging between calls:
+ * a repeated call of the same size adds none); -1 if it has no worker yet. */
+int64_t lz4ada_multi_device_allocs(int device);
+/* The RCCL version the process actually bound (ncclGetVersion, e.g. 22606
+ * for 2.26.6): in a process that loaded another librccl.so.1 first (a torch
+ * job loads its bundled one), that library serves this one's calls too;
+ * a plain C / Ada program gets /opt/rocm/lib's (the library's RUNPATH). */
+int lz4ada_rccl_version(void);
 
 /* ------------------------------------------------------------------ misc */
 

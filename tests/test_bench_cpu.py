@@ -42,3 +42,34 @@ def test_shard_ranges_cover_frame(world, total):
     assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
     sizes = [hi - lo for lo, hi in rs]
     assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("first,nblocks,unique", [(0, 10, 4), (3, 10, 4), (5, 3, 8), (0, 64, 64),
+                                                  (7, 130, 64)])
+def test_assemble_shard_device_tiling(first, nblocks, unique):
+    """The shard is one period of unique blocks tiled on the device: bytes
+    and descriptors must equal a plain host assembly of the same blocks."""
+    import random
+    import torch
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "bo-lz4-ada_amd"))
+    import lz4ada
+    rng = random.Random(first * 1000 + nblocks)
+    recs = []
+    for i in range(unique):
+        clen = rng.randrange(5, 300)
+        rec = (clen).to_bytes(4, "little") + bytes(rng.randrange(256) for _ in range(clen)) + \
+            rng.randrange(1 << 32).to_bytes(4, "little")
+        recs.append((rec, clen, 1000 + i, rng.randrange(1 << 32), b"", b""))
+    fr, fl, de, eh, cb, rb, descs = bench.assemble_shard(lz4ada, torch, recs, first, nblocks, 4096,
+                                                         torch.device("cpu"))
+    want = b"".join(recs[(first + i) % unique][0] for i in range(nblocks)) + bytes(64)
+    assert fl == len(want) and bytes(fr.numpy().tobytes()) == want
+    pos = 0
+    for i in range(nblocks):
+        r = recs[(first + i) % unique]
+        assert descs[i].in_off == pos + 4 and descs[i].in_len == r[1]
+        assert descs[i].cksum == int.from_bytes(r[0][4 + r[1]:], "little")
+        assert descs[i].flags == lz4ada.BLOCK_HAS_CKSUM
+        pos += len(r[0])
+    assert eh == [recs[(first + i) % unique][3] for i in range(nblocks)]

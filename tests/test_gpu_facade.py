@@ -180,3 +180,47 @@ def test_facade_legacy_readahead():
         for feed in (0, 4096):
             assert trace_ours(data, feed, lz4ada.FOR_ALL) == \
                 trace_oracle(data, feed, O.FOR_ALL), (name, feed)
+
+
+def test_facade_async_hash_then_readahead_same_buffer():
+    """a 4 MiB block delivered alone hands its content hash
+    to a helper thread; the next call serves the following blocks from the
+    read-ahead batch into the same Buffer range (Output_Pos restarts at 0).
+    The copy must wait for the hash, or a valid frame fails its content
+    checksum."""
+    frame, raw = synth((1, 0, 2), 5, 4 << 20, seed=21, indep=True, block_cksum=False,
+                       content_cksum=True)
+    info, descs = lz4ada.frame_index(frame)
+    # first call: up to the end of block 0 exactly; second: everything else
+    first_end = descs[0].in_off + descs[0].in_len
+    for rep in range(3):
+        ctx, pos, mbs = lz4ada.Decompressor.init_with_header(frame)
+        buf = bytearray(mbs)
+        out = bytearray()
+        stop = first_end
+        while pos < len(frame):
+            c, f, l = ctx.update(frame, buf, pos, stop)
+            out += buf[f:l + 1] if l >= f else b""
+            pos += c
+            stop = len(frame)
+            if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
+                break
+        assert bytes(out) == raw, rep
+
+
+def test_facade_buffer_far_larger_than_block_max():
+    """the lone decoder's slot is sized by the frame's block
+    maximum, not by the caller's Buffer (a 1.5 GiB Buffer asked the device
+    for 4x its size, and over 1 GiB the launch failed as a device error)."""
+    frame, raw = synth((1, 0), 4, 1 << 20, seed=23, indep=True, block_cksum=True,
+                       content_cksum=True)
+    ctx, pos, mbs = lz4ada.Decompressor.init_with_header(frame)
+    buf = bytearray(max(mbs, 3 << 29))
+    out = bytearray()
+    while pos < len(frame):
+        c, f, l = ctx.update(frame, buf, pos, min(len(frame), pos + (1 << 20) + 100))
+        out += buf[f:l + 1] if l >= f else b""
+        pos += c
+        if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
+            break
+    assert bytes(out) == raw

@@ -115,3 +115,26 @@ def test_multi_repeated_calls_reuse_workers():
     frame, raw = indep_frame([4 << 20] * 4, 4 << 20, block_cksum=True)
     for _ in range(5):
         assert lz4ada.decode_frame_multi(frame, 1)[0] == raw
+
+
+def test_multi_repeated_call_allocates_nothing():
+    """the worker keeps its device buffers and pinned
+    staging across calls -- a repeated call of the same frame makes no new
+    device allocation -- and the H2D runs in pinned chunks beside the
+    decode (a frame over the 64 MiB staging chunk spans several groups)."""
+    frame, raw = indep_frame([4 << 20] * 40 + [777], 4 << 20, block_cksum=True,
+                             content_cksum=True)
+    out, cons = lz4ada.decode_frame_multi(frame, 1)
+    assert out == raw
+    n0 = lz4ada.multi_device_allocs(0)
+    assert n0 > 0
+    for _ in range(2):
+        out, cons = lz4ada.decode_frame_multi(frame, 1)
+        assert out == raw and cons == len(frame)
+    assert lz4ada.multi_device_allocs(0) == n0
+
+
+def test_rccl_version_reported():
+    v = lz4ada.rccl_version()
+    assert v >= 20000, v
+    print("RCCL bound in this process:", v)

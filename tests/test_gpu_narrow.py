@@ -163,3 +163,20 @@ def test_d1_block_mid_frame_resumes_there():
     st, exc = check_like_oracle(frame)
     assert st == O.OK
     assert lz4ada.last_path() == lz4ada.PATH_LINKED | lz4ada.PATH_EXACT
+
+
+def test_bulk_resume_checks_declared_content_size():
+    """blocks before a failing one that already decode past the
+    declared content size -- the reference raises the content-size error in
+    the first block that overruns (lz4ada.adb:830-835), not the later
+    block's checksum error."""
+    blocks = [lz4ada.gen_block(1, 300 + i, 256 << 10) + (False,) for i in range(8)]
+    frame, raw = lz4frame.build_frame(blocks, 256 << 10, indep=True, block_cksum=True,
+                                      content_cksum=True, with_content_size=True)
+    hdr_len = len(lz4frame.header(256 << 10, True, True, True, len(raw)))
+    hdr = lz4frame.header(256 << 10, True, True, True, 3 * (256 << 10) + 1000)
+    small = bytearray(hdr + frame[hdr_len:])
+    info, descs = lz4ada.frame_index(bytes(small))
+    small[descs[6].in_off + 40] ^= 0x5A  # block 6's checksum fails
+    st, exc = check_like_oracle(bytes(small))
+    assert isinstance(exc, lz4ada.DataCorruption) and "content size" in str(exc)

@@ -21,8 +21,11 @@ import glob
 import json
 import os
 import shutil
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import kernel_src_hash  # noqa: E402
 KERNELS = ("k_decode_idx", "k_index", "k_decode_sparse", "k_decode_pc", "k_decode_wg", "k_decode_blocks",
            "k_xxh32_rows", "k_serial_block", "k_xxh32_update",
            "k_compact")
@@ -140,6 +143,8 @@ def main():
               "fetch_bytes_x2": round(dec["fetch_bytes_x2"]),
               "write_bytes": round(dec["write_bytes"]),
               "avg_ns": dec.get("avg_ns"),
+              # bench.py reuses the figure only while the kernel sources match
+              "kernel_src_sha16": kernel_src_hash(),
               "source": f"profiles/{args.tag}_pmc.json (tools/profile.sh + tools/pmc_summary.py)"}
         with open(os.path.join(prof, "pmc_decode.json"), "w") as fh:
             json.dump(pj, fh, indent=1)
