@@ -69,7 +69,10 @@ struct SerialState {
 
 // Bulk independent-block decoders (LZ4ADA_DECODE_* in lz4ada_hip.h).
 enum DecVariant : int { DEC_PC = 0, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4,
-                        DEC_IDX_LINKED = 5, DEC_IDX_SPARSE = 6 };
+                        DEC_IDX_LINKED = 5, DEC_IDX_SPARSE = 6,
+                        // the fused index decoder alone with one / two waves per block
+                        DEC_IDX1_ALONE = 7, DEC_IDX2_ALONE = 8 };
+int idx_fused_mode();  // 3: k_decode_idx, 4: k_decode_idx2 (lz4ada_idx.hip)
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,

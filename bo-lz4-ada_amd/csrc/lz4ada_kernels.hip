@@ -1401,6 +1401,9 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 	}
 	if (variant == DEC_IDX_LINKED)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream, 1);
+	if (variant == DEC_IDX1_ALONE || variant == DEC_IDX2_ALONE)
+		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream,
+		                         variant == DEC_IDX1_ALONE ? -1 : -2);
 	if (variant == DEC_IDX || variant == DEC_IDX_ALONE || variant == DEC_IDX_SPARSE) {
 		const hipError_t err = launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out,
 		                                         d_status, stream);
@@ -1539,7 +1542,8 @@ hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
 	static const bool fuse = getenv("LZ4ADA_NO_FUSE") == nullptr;
 	if (err == hipSuccess)
 		err = fuse ? launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
-		                                   static_cast<const uint8_t*>(tab), d_out, d_status, 3, stream)
+		                                   static_cast<const uint8_t*>(tab), d_out, d_status,
+		                                   idx_fused_mode(), stream)
 		           : launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab),
 		                          d_status, stream);
 	if (err == hipSuccess)

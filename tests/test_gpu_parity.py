@@ -276,7 +276,7 @@ def test_device_resident_blocks():
 
 # ------------------------------------------- bench-sized blocks (regression)
 
-@pytest.mark.parametrize("variant", ["pc", "wg", "idx"])
+@pytest.mark.parametrize("variant", ["pc", "wg", "idx", "idx1"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
 def test_bench_blocks_exact(kind, variant):
     """The bench's own unique 4 MiB blocks (seed 0x4C5A3441 + i) decode
@@ -297,7 +297,7 @@ def test_bench_blocks_exact(kind, variant):
     sh = torch.cuda.current_stream().cuda_stream
     lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), nb, d_st.data_ptr(), sh)
     v = {"pc": lz4ada.DECODE_PC, "wg": lz4ada.DECODE_WG,
-         "idx": lz4ada.DECODE_IDX}[variant]
+         "idx": lz4ada.DECODE_IDX, "idx1": lz4ada.DECODE_IDX1_ALONE}[variant]
     lz4ada.launch_decode_variant(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
                                  d_out.data_ptr(), d_st.data_ptr(), v, sh)
     torch.cuda.synchronize()
@@ -419,9 +419,10 @@ def _run_variant_alone(frame, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "rle"])
+@pytest.mark.parametrize("variant", ["default", "idx1", "idx2"])
+@pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "rle", "chain"])
 @pytest.mark.parametrize("bmax", [64 << 10, 256 << 10, 4 << 20])
-def test_idx_decoder_alone(kind, bmax):
+def test_idx_decoder_alone(kind, bmax, variant):
     """k_index + k_decode_idx on their own: exact output for every block they
     accept, and they accept every well-formed independent block except sparse
     large ones (long literal runs: over 64 input bytes per sequence), which
@@ -429,8 +430,13 @@ def test_idx_decoder_alone(kind, bmax):
     at least 4 KiB input with over 64 output bytes (slot) per input byte."""
     blocks = [lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 0x4C5A3441 + i, bmax) for i in range(6)]
     blocks.append(lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 77, 1000))  # short last block
+    # ragged sizes: partial pass-1 chunks and batches, both waves' shares
+    for j, n in enumerate((bmax - 1, bmax // 2 + 33, 16384 + 5, 4097, 200, 17, 1)):
+        blocks.append(lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 900 + j, min(n, bmax)))
     frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, indep=True)
-    descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX_ALONE)
+    v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
+         "idx2": lz4ada.DECODE_IDX2_ALONE}[variant]
+    descs, st, out = _run_variant_alone(frame, v)
     bad = []
     for i, (c, r) in enumerate(blocks):
         if kind == "literal" and st[i].code == lz4ada.DS_SPARSE and len(c) >= 65536:
@@ -487,16 +493,23 @@ def oracle_blocks(frame, nblocks):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("alone", ["default", "idx1", "idx2"])
 @pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
-def test_idx_decoder_on_vectors(name, digests):
+def test_idx_decoder_on_vectors(name, digests, alone):
     """Reference vectors' blocks through the idx decoder (+ retry): every block
     byte-exact; linked blocks that reference earlier blocks are declined
     (DS_RETRY) by the idx pass and redone exactly."""
     frame = read_vector(name, "lz4")
     info, _ = lz4ada.frame_index(frame)
-    descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX_ALONE)
+    v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
+         "idx2": lz4ada.DECODE_IDX2_ALONE}[alone]
+    descs, st, out = _run_variant_alone(frame, v)
     for i in range(info.nblocks):
         assert st[i].code in (0, lz4ada.DS_RETRY, lz4ada.DS_SPARSE), (i, st[i].code)
+    ref = oracle_blocks(frame, info.nblocks)
+    for i in range(info.nblocks):  # every block the index decoder alone took
+        if st[i].code == 0:
+            assert out[i * info.block_max:i * info.block_max + st[i].out_len] == ref[i], i
     descs, st, out = _run_variant_alone(frame, lz4ada.DECODE_IDX)
     pieces = [out[i * info.block_max:i * info.block_max + st[i].out_len]
               for i in range(info.nblocks)]
