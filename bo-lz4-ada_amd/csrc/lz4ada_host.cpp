@@ -404,6 +404,30 @@ static bool decode_lone_blocks(const uint8_t* host_in, const uint8_t* d_in,
                                const std::vector<lz4ada_block_desc>& d, uint8_t* d_out,
                                lz4ada_block_status* d_st, std::vector<lz4ada_block_status>& st,
                                DevBuf<uint8_t>& scr, hipStream_t stream);
+enum BulkResult { BULK_OK, BULK_EXACT, BULK_PRE_REF, BULK_FAIL_AT };
+// Where a linked batch's resolved bytes go: dst(n) returns the device
+// buffer for the batch's n bytes (nullptr: no room), done(p, n) runs once
+// they are there.
+struct LinkedSink {
+	std::function<uint8_t*(int64_t)> dst;
+	std::function<void(const uint8_t*, int64_t)> done;
+};
+
+// A linked batch that starts mid-frame (the facade's read-ahead): the
+// history before its first block, as device bytes oldest first (the
+// reference's Buffer keeps it in two places), and the reference's
+// Output_Pos / Output_Pos_History there (quirk D1).
+struct LinkedHist {
+	const uint8_t* h0 = nullptr;
+	int64_t n0 = 0;
+	const uint8_t* h1 = nullptr;
+	int64_t n1 = 0;
+	int64_t output_pos = 0, output_pos_history = 0;
+};
+static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block_max,
+                              const std::vector<lz4ada_block_desc>& descs, LinkedSink& sink,
+                              uint64_t& total, std::vector<uint32_t>& lens, int64_t& fail,
+                              hipStream_t stream, const LinkedHist* hist = nullptr);
 }  // namespace lz4ada
 
 struct lz4ada_decompressor {
@@ -414,6 +438,7 @@ struct lz4ada_decompressor {
 	int64_t output_pos_history = 0;
 	int64_t input_length = -1;
 	std::string err;
+	int64_t exact_blocks = 0;  // blocks decoded by the reference-exact serial kernel (diagnostics)
 
 	// device side (lazily created at the first block)
 	bool dev_ready = false;
@@ -703,6 +728,7 @@ struct lz4ada_decompressor {
 		s.size_remaining = m.size_remaining;
 		s.has_content_size = m.has_content_size ? 1 : 0;
 		HIP_OK(hipMemcpyAsync(d_serial.p, &s, sizeof s, hipMemcpyHostToDevice, stream));
+		++exact_blocks;
 		HIP_OK(launch_serial_block(d_buf.p, buflen, d_blk.p, raw_len,
 		                           m.is_compressed ? raw_len : blen, m.is_compressed ? 1 : 0,
 		                           d_serial.p, stream));
@@ -764,6 +790,8 @@ struct lz4ada_decompressor {
 			return DEC_PC;
 		if (e && !strcmp(e, "wg"))
 			return DEC_WG;
+		if (e && !strcmp(e, "lone"))
+			return -2;  // the lone-block decoder at every size
 		return -1;  // lone (large blocks), else wg
 	}
 
@@ -795,15 +823,49 @@ struct lz4ada_decompressor {
 		return cap;
 	}
 
+	// The history a block of a linked frame may read (lz4ada.adb:678-690,
+	// 862-883) when it starts at Buffer position `start`: the current round's
+	// bytes Buffer(0 .. start-1) (n1), and before them the previous round's
+	// tail Buffer(OPH - n0 .. OPH - 1) -- up to 65535 bytes in all, the
+	// largest offset.  Before the first round ends there is none beyond n1.
+	void history_of(int64_t start, int64_t& n0, int64_t& n1) const
+	{
+		n1 = start;
+		n0 = std::min<int64_t>(65535, start + output_pos_history) - n1;
+	}
+	// Quirk D1 can only strike right after a round that ended within the
+	// reference's 8-byte wild copy of 64 KiB (lz4ada.adb:811-817, 862-879).
+	bool d1_window() const
+	{
+		return output_pos_history >= HISTORY_SIZE && output_pos_history <= HISTORY_SIZE + 6;
+	}
+
 	int64_t launch_fast_block(int64_t raw_len, int64_t blen, int64_t buflen)
 	{
 		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
-		if (linked || getenv("LZ4ADA_FACADE_EXACT"))
+		if (getenv("LZ4ADA_FACADE_EXACT"))
 			return -1;
 		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;  // :678-680
 		if (buflen - start <= 0 || raw_len > INT32_MAX)
 			return -1;
 		const int64_t cap = std::max<int64_t>(block_room(buflen - start, raw_len, m.is_compressed), 1);
+		if (linked && m.is_compressed) {
+			// a linked frame's block: the lone-block decoder with the
+			// reference's history as readable words in front of its output
+			// (every block size; a reference past the history, D1 risk or any
+			// other decline leaves it to the exact path)
+			if (raw_len <= 0 || cap > (int64_t(1) << 30))
+				return -1;
+			int64_t n0, n1;
+			history_of(start, n0, n1);
+			const int64_t sb = lone_scratch_bytes(raw_len, cap);
+			d_scr.reserve(size_t(cap));
+			d_lone.reserve(size_t(sb));
+			HIP_OK(launch_decode_lone(d_blk.p, raw_len, d_scr.p, cap, d_bst.p, d_lone.p, sb, stream,
+			                          d_buf.p + output_pos_history - n0, int32_t(n0), d_buf.p,
+			                          int32_t(n1), d1_window() ? 1 : 0));
+			return start;
+		}
 		d_scr.reserve(size_t(cap));
 		lz4ada_block_desc d{};
 		d.in_off = 0;
@@ -812,7 +874,8 @@ struct lz4ada_decompressor {
 		d.out_off = 0;
 		d.out_cap = uint32_t(cap);
 		const int fv = facade_variant();
-		if (fv < 0 && m.is_compressed && raw_len >= LONE_MIN && cap <= (int64_t(1) << 30)) {
+		if (fv < 0 && m.is_compressed && (raw_len >= LONE_MIN || fv == -2) && raw_len > 0 &&
+		    cap <= (int64_t(1) << 30)) {
 			const int64_t sb = lone_scratch_bytes(raw_len, cap);
 			d_lone.reserve(size_t(sb));
 			HIP_OK(launch_decode_lone(d_blk.p, raw_len, d_scr.p, cap, d_bst.p, d_lone.p, sb, stream));
@@ -855,8 +918,7 @@ struct lz4ada_decompressor {
 		ahead.clear();
 		if (m.is_format != F_MODERN && m.is_format != F_LEGACY)
 			return false;
-		if (m.is_format == F_MODERN && !(m.flg & 0x20u))
-			return false;  // linked frame: every block needs the history (exact path)
+		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
 		const int bcl = m.block_checksum_length;
 		const int64_t avail = end - blk;
 		// a slot holds one block: the Buffer's room, at most the block maximum
@@ -912,6 +974,8 @@ struct lz4ada_decompressor {
 		HIP_OK(hipMemcpyAsync(ahead.d_desc.p, ahead.descs.data(), nb * sizeof(lz4ada_block_desc),
 		                      hipMemcpyHostToDevice, stream));
 		HIP_OK(hipMemsetAsync(ahead.d_st.p, 0, nb * sizeof(lz4ada_block_status), stream));
+		if (linked)
+			return build_ahead_linked(nb, pos, buflen);
 		if (few_large_blocks(ahead.descs) &&
 		    decode_lone_blocks(blk, ahead.d_in.p, ahead.descs, ahead.d_out.p, ahead.d_st.p, ahead.st,
 		                       ahead.d_lone, stream))
@@ -925,6 +989,58 @@ struct lz4ada_decompressor {
 		HIP_OK(hipMemcpyAsync(ahead.st.data(), ahead.d_st.p, nb * sizeof(lz4ada_block_status),
 		                      hipMemcpyDeviceToHost, stream));
 		HIP_OK(hipStreamSynchronize(stream));
+		return true;
+	}
+
+	// Read-ahead of a linked frame's blocks: all of them at once against
+	// synthetic history, resolved on the GPU (bulk_linked, §7 of DESIGN),
+	// seeded with the reference's history before the first one and its
+	// Output_Pos / Output_Pos_History (quirk D1).  The blocks up to the
+	// first one it cannot take are served; that one goes to the exact path.
+	bool build_ahead_linked(size_t nb, int64_t in_len, int64_t buflen)
+	{
+		if (buflen > d_buf_len)
+			grow_mirror(buflen);
+		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;
+		LinkedHist lh;
+		history_of(start, lh.n0, lh.n1);
+		lh.h0 = d_buf.p + output_pos_history - lh.n0;
+		lh.h1 = d_buf.p;
+		lh.output_pos = output_pos;
+		lh.output_pos_history = output_pos_history;
+		const int64_t bmax = int64_t(1) << (8 + 2 * ((m.bd & 0x70u) >> 4));
+		int64_t room = 0;
+		for (const auto& d : ahead.descs)
+			room += std::max<int64_t>(d.out_cap, 1);
+		ahead.d_out.reserve(size_t(room));
+		int64_t used = 0;
+		LinkedSink ls;
+		ls.dst = [&](int64_t n) -> uint8_t* { return used + n <= room ? ahead.d_out.p + used : nullptr; };
+		ls.done = [&](const uint8_t*, int64_t n) { used += n; };
+		uint64_t total = 0;
+		std::vector<uint32_t> lens;
+		int64_t fail = -1;
+		const BulkResult r = bulk_linked(ahead.d_in.p, uint64_t(in_len), bmax, ahead.descs, ls, total, lens,
+		                                 fail, stream, &lh);
+		HIP_OK(hipStreamSynchronize(stream));
+		if (r != BULK_OK && r != BULK_FAIL_AT) {
+			ahead.clear();
+			return false;  // each block alone (lone decoder with history, else exact)
+		}
+		uint64_t off = 0;
+		for (size_t k = 0; k < nb; ++k) {
+			lz4ada_block_status& st = ahead.st[k];
+			st = lz4ada_block_status{};
+			if (k < lens.size()) {
+				st.code = DS_OK;
+				st.out_len = lens[k];
+				st.cksum = ahead.descs[k].cksum;  // checked by bulk_linked
+				ahead.descs[k].out_off = off;
+				off += lens[k];
+			} else {
+				st.code = DS_RETRY;
+			}
+		}
 		return true;
 	}
 
@@ -1116,6 +1232,8 @@ const char* lz4ada_error_name(int status)
 const char* lz4ada_thread_last_error(void) { return g_thread_error.c_str(); }
 
 const char* lz4ada_last_error(const lz4ada_decompressor* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int64_t lz4ada_exact_blocks(const lz4ada_decompressor* ctx) { return ctx ? ctx->exact_blocks : -1; }
 
 int lz4ada_device_check(void)
 {
@@ -1576,7 +1694,8 @@ static bool try_reserve(DevBuf<T>& b, size_t count)
 // and a first-touch each time otherwise -- more than the decode itself on a
 // 1 GiB linked frame.  lz4ada_release_device_cache() frees them.  The
 // cache is never destroyed at thread exit (the HIP runtime may be gone).
-enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_TAB, SC_P, SC_F, SC_LONE, SC_N };
+enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_TAB, SC_P, SC_F, SC_LONE, SC_U, SC_L,
+	                  SC_N };
 struct ScratchCache {
 	DevBuf<uint8_t> b[SC_N];
 };
@@ -1713,8 +1832,6 @@ static std::vector<std::pair<uint32_t, uint32_t>> batches_of(const std::vector<l
 	return v;
 }
 
-enum BulkResult { BULK_OK, BULK_EXACT, BULK_PRE_REF, BULK_FAIL_AT };
-
 // Independent blocks, batch by batch: block checksums + the bulk decoder
 // over slots, then the batch's bytes (compacted if a block is short) to the
 // sink, hashed on the way when the frame has a content checksum.
@@ -1821,13 +1938,6 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const uint8_t* host_f
 	return BULK_OK;
 }
 
-// Where a linked batch's resolved bytes go: dst(n) returns the device
-// buffer for the batch's n bytes (nullptr: no room), done(p, n) runs once
-// they are there.
-struct LinkedSink {
-	std::function<uint8_t*(int64_t)> dst;
-	std::function<void(const uint8_t*, int64_t)> done;
-};
 
 static void d2h(void* dst, const void* src, size_t n, hipStream_t stream)
 {
@@ -1844,7 +1954,7 @@ static void d2h(void* dst, const void* src, size_t n, hipStream_t stream)
 static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block_max,
                               const std::vector<lz4ada_block_desc>& descs, LinkedSink& sink,
                               uint64_t& total, std::vector<uint32_t>& lens, int64_t& fail,
-                              hipStream_t stream)
+                              hipStream_t stream, const LinkedHist* hist)
 {
 	lens.clear();
 	fail = -1;
@@ -1871,6 +1981,18 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 	// the reference's Output_Pos / Output_Pos_History (lz4ada.adb:678-690,
 	// 785-787), for quirk D1
 	int64_t opos = 0, oph = 0;
+	int64_t hist0 = 0;  // history bytes before the first block (mid-frame batch)
+	if (hist) {
+		hist0 = std::min<int64_t>(hist->n0 + hist->n1, HISTORY_SIZE);
+		if (hist->n1 > 0)
+			HIP_OK(hipMemcpyAsync(d_tail[0].p + HISTORY_SIZE - hist->n1, hist->h1, size_t(hist->n1),
+			                      hipMemcpyDeviceToDevice, stream));
+		if (hist->n0 > 0)
+			HIP_OK(hipMemcpyAsync(d_tail[0].p + HISTORY_SIZE - hist->n1 - hist->n0, hist->h0,
+			                      size_t(hist->n0), hipMemcpyDeviceToDevice, stream));
+		opos = hist->output_pos;
+		oph = hist->output_pos_history;
+	}
 	uint32_t lo = 0;
 	total = 0;
 	while (lo < descs.size()) {
@@ -1977,26 +2099,58 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		d_ctr.reserve(2);
 		HIP_OK(hipMemcpyAsync(d_A.p, A.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
 		HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
-		HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p,
-		                        d_ctr.p, stream));
+		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
 		uint32_t ctr[2] = { 0, 0 };
-		d2h(ctr, d_ctr.p, sizeof ctr, stream);
-		phase("init");
-		const int64_t tail_valid = std::min<int64_t>(int64_t(total), HISTORY_SIZE);
-		for (int round = 0; ctr[0] > 0; ++round) {
-			if (round > 64)
-				return BULK_EXACT;  // never expected: every pointer goes strictly back
-			HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
-			HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, d_ctr.p, stream));
+		uint8_t* F = nullptr;
+		// sparse resolution (default): only history-derived bytes are jumped;
+		// LZ4ADA_LINKED_DENSE=1 keeps a word per output byte (round 2-3 form)
+		static const bool dense = getenv("LZ4ADA_LINKED_DENSE") != nullptr;
+		if (!dense) {
+			F = sink.dst(n);
+			struct {
+				uint8_t* p;
+			} d_U{ F ? scratch(SC_U, size_t((n + 63) / 32 * 4 + 64)) : nullptr },
+			    d_L{ d_U.p ? scratch(SC_L, size_t(std::max<int64_t>(n, 1)) * 4) : nullptr };
+			if (!d_L.p)
+				return BULK_EXACT;
+			uint32_t* U = reinterpret_cast<uint32_t*>(d_U.p);
+			uint32_t* Lst = reinterpret_cast<uint32_t*>(d_L.p);
+			HIP_OK(hipMemsetAsync(U, 0, size_t((n + 63) / 32 * 4 + 64), stream));
+			HIP_OK(launch_link_init2(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, U, F,
+			                         Lst, d_ctr.p, stream));
 			d2h(ctr, d_ctr.p, sizeof ctr, stream);
-			if (ctr[1])
-				return BULK_EXACT;  // a reference before the frame start: the exact error
+			phase("init2");
+			const int64_t nl = ctr[0];
+			for (int round = 0; ctr[0] > 0; ++round) {
+				if (round > 64)
+					return BULK_EXACT;  // never expected: every pointer goes strictly back
+				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
+				HIP_OK(launch_link_jump2(d_P.p, U, F, Lst, nl, d_tail[cur].p, tail_valid, d_ctr.p, stream));
+				d2h(ctr, d_ctr.p, sizeof ctr, stream);
+				if (ctr[1])
+					return BULK_EXACT;  // a reference before the frame start: the exact error
+			}
+			phase("jumps2");
+		} else {
+			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p,
+			                        d_ctr.p, stream));
+			d2h(ctr, d_ctr.p, sizeof ctr, stream);
+			phase("init");
+			for (int round = 0; ctr[0] > 0; ++round) {
+				if (round > 64)
+					return BULK_EXACT;  // never expected: every pointer goes strictly back
+				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
+				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, d_ctr.p, stream));
+				d2h(ctr, d_ctr.p, sizeof ctr, stream);
+				if (ctr[1])
+					return BULK_EXACT;  // a reference before the frame start: the exact error
+			}
+			F = sink.dst(n);
+			if (!F)
+				return BULK_EXACT;
+			phase("jumps");
+			HIP_OK(launch_link_emit(d_P.p, n, F, stream));
 		}
-		uint8_t* F = sink.dst(n);
-		if (!F)
-			return BULK_EXACT;
-		phase("jumps");
-		HIP_OK(launch_link_emit(d_P.p, n, F, stream));
 		HIP_OK(launch_link_tail(F, n, d_tail[cur].p, d_tail[cur ^ 1].p, stream));
 		cur ^= 1;
 		phase("emit");

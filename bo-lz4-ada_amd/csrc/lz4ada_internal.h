@@ -171,6 +171,16 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h
                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
                             uint32_t* d_ctr, hipStream_t stream);
+// Sparse resolution: constants straight to F, pointer words, U bits and
+// list entries only for history-derived bytes; jumping over the list.
+hipError_t launch_link_init2(const uint8_t* x, const uint8_t* y, const uint8_t* h,
+                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
+                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
+                             uint32_t* d_U, uint8_t* d_F, uint32_t* d_L, uint32_t* d_ctr,
+                             hipStream_t stream);
+hipError_t launch_link_jump2(uint32_t* d_P, const uint32_t* d_U, uint8_t* d_F, const uint32_t* d_L,
+                             int64_t nl, const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_ctr,
+                             hipStream_t stream);
 hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
                             uint32_t* d_ctr, hipStream_t stream);
 hipError_t launch_link_emit(const uint32_t* d_P, int64_t n, uint8_t* d_F, hipStream_t stream);
@@ -180,11 +190,16 @@ hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail
 // Gather variable-length slots into a contiguous buffer (short blocks).
 // One block decoded by the whole GPU (lz4ada_lone.hip): d_st gets DS_OK and
 // out_len, or DS_RETRY (the exact path then decides).  d_scratch holds
-// lone_scratch_bytes(n, cap) bytes.
+// lone_scratch_bytes(n, cap) bytes.  History (a linked frame's block): the
+// n0 + n1 <= 65535 bytes before the block, h0 then h1 (device memory; the
+// reference's Buffer keeps them in two places), readable by its matches;
+// d1_guard: a match reaching >= D1_OFF back before the block start declines
+// it (quirk D1).  Without history such a match declines it.
 int64_t lone_scratch_bytes(int64_t n, int64_t cap);
 hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
                               lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
-                              hipStream_t stream);
+                              hipStream_t stream, const uint8_t* d_h0 = nullptr, int32_t n0 = 0,
+                              const uint8_t* d_h1 = nullptr, int32_t n1 = 0, int d1_guard = 0);
 
 // host side (lz4ada_host.cpp): the calling thread's message for
 // lz4ada_thread_last_error() and its lz4ada_last_path() bits

@@ -452,7 +452,7 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
 // copies).  Threads j = j0, j0 + js, ... of the caller share the work.
 __device__ __forceinline__ void lone_emit(const LoneSrc& S, const LoneSeq& q, uint32_t o,
                                           uint32_t* __restrict__ W, int32_t j0, int32_t js,
-                                          int32_t n)
+                                          int32_t n, uint32_t hb)
 {
 	for (int32_t b = 4 * j0; b < q.L; b += 4 * js) {
 		const int32_t x = q.lit + b;
@@ -472,7 +472,7 @@ __device__ __forceinline__ void lone_emit(const LoneSrc& S, const LoneSeq& q, ui
 	}
 	const uint32_t m0 = o + uint32_t(q.L);
 	for (int32_t b = j0; b < q.ml; b += js)
-		W[m0 + uint32_t(b)] = m0 + uint32_t(b) - uint32_t(q.off);
+		W[m0 + uint32_t(b)] = hb + m0 + uint32_t(b) - uint32_t(q.off);
 }
 
 __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ blk, int32_t n,
@@ -481,8 +481,11 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
                                                    const uint32_t* __restrict__ obase,
                                                    LoneCtl* __restrict__ ctl,
                                                    lz4ada_block_status* __restrict__ st,
-                                                   uint32_t* __restrict__ W)
+                                                   uint32_t* __restrict__ Wbase, int32_t H,
+                                                   int32_t d1_guard)
 {
+	// words [0, H): the history (literals); output byte x is word H + x
+	uint32_t* __restrict__ W = Wbase + H;
 	__shared__ alignas(16) uint8_t s[LSTG + 32];
 	__shared__ uint16_t J[LW];
 	__shared__ uint8_t mark[LW];
@@ -566,8 +569,10 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 		const LoneSeq& q = qs[k];
 		if (q.nx == NX_BAD)
 			bad = true;  // never expected: k_lone_chain accepted this chain
-		else if (q.ml && int64_t(o) + q.L < int64_t(q.off))
-			bad = true;  // a reference before the block start: history (exact path)
+		else if (q.ml && int64_t(o) + q.L + H < int64_t(q.off))
+			bad = true;  // a reference before the history it was given (exact path)
+		else if (d1_guard && q.ml && int64_t(o) + q.L < int64_t(q.off) && q.off >= D1_OFF)
+			bad = true;  // quirk D1: the reference's wild copy may have clobbered it
 		else if (int32_t(q.os) > LONG_SEQ) {
 			const int32_t i = atomicAdd(&nlong, 1);
 			if (i < LW / 4) {
@@ -577,7 +582,7 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 				bad = true;  // never expected (a window holds < LW/4 long sequences)
 			}
 		} else {
-			lone_emit(S, q, o, W, 0, 1, n);
+			lone_emit(S, q, o, W, 0, 1, n, uint32_t(H));
 		}
 		o += q.os;
 	}
@@ -593,7 +598,7 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 	const int32_t nl = nlong;
 	for (int32_t i = 0; i < nl; ++i) {
 		const LoneSeq q = lone_parse(S, lpos[i], n, GMAX_TRUE);
-		lone_emit(S, q, lout[i], W, tid, LT, n);
+		lone_emit(S, q, lout[i], W, tid, LT, n, uint32_t(H));
 	}
 }
 
@@ -616,7 +621,7 @@ constexpr int32_t RPT = RES_SLICE / LT;  // words per thread (64)
 __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
                                                      const LoneCtl* __restrict__ ctl,
                                                      lz4ada_block_status* __restrict__ st,
-                                                     uint8_t* __restrict__ out)
+                                                     uint8_t* __restrict__ out, uint32_t H)
 {
 	if (ctl->code != DS_OK)
 		return;
@@ -633,7 +638,7 @@ __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
 		const uint32_t i = base + 4u * (tid + uint32_t(LT) * uint32_t(k));
 #pragma unroll
 		for (int32_t j = 0; j < 4; ++j)
-			v[4 * k + j] = (i + uint32_t(j) < total) ? W[i + uint32_t(j)] : LIT;
+			v[4 * k + j] = (i + uint32_t(j) < total) ? W[H + i + uint32_t(j)] : LIT;
 	}
 	int pend = 1;
 	for (int32_t round = 0; round < 1024 && pend; ++round) {
@@ -643,7 +648,7 @@ __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
 #pragma unroll
 		for (int32_t k = 0; k < RPT; ++k) {
 			const uint32_t i = base + 4u * (tid + uint32_t(LT) * uint32_t(k >> 2)) + uint32_t(k & 3);
-			const uint32_t a = (v[k] & LIT) ? min(i, total - 1) : v[k];
+			const uint32_t a = (v[k] & LIT) ? H + min(i, total - 1) : v[k];
 			nv[k] = w_load(W + a);
 		}
 		pend = 0;
@@ -654,7 +659,7 @@ __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
 				v[k] = nv[k];
 				pend |= !(nv[k] & LIT);
 				if (i < total)
-					w_store(W + i, v[k]);
+					w_store(W + H + i, v[k]);
 			}
 		}
 		pend = __syncthreads_or(pend);
@@ -682,21 +687,36 @@ __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
 	}
 }
 
+// History words: the H bytes before the block (a linked frame's earlier
+// output) as literals, so matches reaching back resolve like any other.
+__global__ __launch_bounds__(LT) void k_lone_hist(uint32_t* __restrict__ W, const uint8_t* __restrict__ h0,
+                                                  int32_t n0, const uint8_t* __restrict__ h1, int32_t n1)
+{
+	const int32_t i = int32_t(blockIdx.x) * LT + int32_t(threadIdx.x);
+	if (i < n0)
+		W[i] = LIT | uint32_t(h0[i]);
+	else if (i < n0 + n1)
+		W[i] = LIT | uint32_t(h1[i - n0]);
+}
+
 // ---------------------------------------------------------------- host side
 int64_t lone_scratch_bytes(int64_t n, int64_t cap)
 {
 	const int64_t nwin = (n + LW - 1) / LW;
 	return 12 * std::max<int64_t>(n, 1) + 12 * (nwin + 2) + 64 + 4 * std::max<int64_t>(cap, 1) +
-	       512;
+	       4 * 65536 + 512;
 }
 
 hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
                               lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
-                              hipStream_t stream)
+                              hipStream_t stream, const uint8_t* d_h0, int32_t n0, const uint8_t* d_h1,
+                              int32_t n1, int d1_guard)
 {
 	const int64_t nwin = (n + LW - 1) / LW;
+	const int32_t H = n0 + n1;
 	if (n <= 0 || n > (int64_t(1) << 30) || cap <= 0 || cap > (int64_t(1) << 30) ||
-	    nwin > CK * CT || scratch_bytes < lone_scratch_bytes(n, cap))
+	    nwin > CK * CT || scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 ||
+	    H > 65535)
 		return hipErrorInvalidValue;
 	uint8_t* sc = static_cast<uint8_t*>(d_scratch);
 	uint32_t* exit_tab = reinterpret_cast<uint32_t*>(sc);
@@ -720,13 +740,21 @@ hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, i
 	err = hipGetLastError();
 	if (err != hipSuccess)
 		return err;
+	if (H > 0) {
+		hipLaunchKernelGGL(k_lone_hist, dim3(uint32_t((H + LT - 1) / LT)), dim3(LT), 0, stream, W, d_h0,
+		                   n0, d_h1, n1);
+		err = hipGetLastError();
+		if (err != hipSuccess)
+			return err;
+	}
 	hipLaunchKernelGGL(k_lone_words, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
-	                   nxt_tab, entry, obase, ctl, d_st, W);
+	                   nxt_tab, entry, obase, ctl, d_st, W, H, d1_guard);
 	err = hipGetLastError();
 	if (err != hipSuccess)
 		return err;
 	const uint32_t nres = uint32_t((cap + RES_SLICE - 1) / RES_SLICE);
-	hipLaunchKernelGGL(k_lone_resolve, dim3(nres), dim3(LT), 0, stream, W, ctl, d_st, d_out);
+	hipLaunchKernelGGL(k_lone_resolve, dim3(nres), dim3(LT), 0, stream, W, ctl, d_st, d_out,
+	                   uint32_t(H));
 	return hipGetLastError();
 }
 

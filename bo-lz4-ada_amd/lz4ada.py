@@ -181,6 +181,7 @@ _sig = {
     "lz4ada_error_name": ([ctypes.c_int], ctypes.c_char_p),
     "lz4ada_thread_last_error": ([], ctypes.c_char_p),
     "lz4ada_last_error": ([_vp], ctypes.c_char_p),
+    "lz4ada_exact_blocks": ([_vp], _i64),
     "lz4ada_init": ([ctypes.c_int, _pi64, _P(_vp)], ctypes.c_int),
     "lz4ada_init_with_header": ([_vp, _i64, ctypes.c_int, _pi64, _pi64, _P(_vp)], ctypes.c_int),
     "lz4ada_init_for_block": ([_i64, ctypes.c_int, _pi64, _P(_vp)], ctypes.c_int),
@@ -345,6 +346,10 @@ class Decompressor:
         if st:
             _check(st, _lib.lz4ada_last_error(self._p).decode())
         return cons.value, first.value, last.value
+
+    def exact_blocks(self) -> int:
+        """Blocks this context decoded on the reference-exact serial path."""
+        return int(_lib.lz4ada_exact_blocks(self._p))
 
     def is_end_of_frame(self) -> EndOfFrame:
         return EndOfFrame(_lib.lz4ada_is_end_of_frame(self._p))

@@ -100,6 +100,11 @@ int lz4ada_is_end_of_frame(const lz4ada_decompressor *ctx);
 /* Exception message of the last failed call on ctx, and the reference
  * exception name for a status ("LZ4ADA.DATA_CORRUPTION"). */
 const char *lz4ada_last_error(const lz4ada_decompressor *ctx);
+/* Blocks this context sent through the reference-exact single-lane path
+ * (k_serial_block: errors, quirk D1, anything the GPU decoders decline);
+ * every other block was decoded by the parallel GPU decoders.  Diagnostic,
+ * no reference twin. */
+int64_t lz4ada_exact_blocks(const lz4ada_decompressor *ctx);
 const char *lz4ada_error_name(int status);
 /* Message of the last failed context-less call on this thread. */
 const char *lz4ada_thread_last_error(void);

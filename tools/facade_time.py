@@ -44,11 +44,18 @@ def main():
     ap.add_argument("--bcksum", type=int, default=1, help="block checksums in the frame")
     ap.add_argument("--ccksum", type=int, default=1, help="content checksum in the frame")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--raw-len", type=int, default=0,
+                    help="decoded bytes per block (default: --block-max)")
     args = ap.parse_args()
-    blocks = []
-    for i in range(args.blocks):
-        comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[args.kind], 0x4C5A3441 + i, args.block_max)
-        blocks.append((comp, raw, False))
+    n = args.raw_len or args.block_max
+    if args.indep:
+        blocks = []
+        for i in range(args.blocks):
+            comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[args.kind], 0x4C5A3441 + i, n)
+            blocks.append((comp, raw, False))
+    else:  # linked: matches reach back into the earlier blocks' output
+        blocks = [(c, r, False) for c, r in
+                  lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS[args.kind], 0x4C5A3441, n, args.blocks)]
     frame, expect = lz4frame.build_frame(blocks, args.block_max, indep=bool(args.indep),
                                          block_cksum=bool(args.bcksum),
                                           content_cksum=bool(args.ccksum))
@@ -56,7 +63,8 @@ def main():
     ts = sorted(run(frame, expect, args.feed) for _ in range(args.reps))
     dt = ts[len(ts) // 2]
     print(f"facade {args.kind} feed={args.feed} bcksum={args.bcksum} ccksum={args.ccksum} "
-          f"{args.blocks}x{args.block_max >> 10} KiB: median of {args.reps} "
+          f"indep={args.indep} {args.blocks}x{n >> 10} KiB (BD {args.block_max >> 10} KiB) "
+          f"decoder={os.environ.get('LZ4ADA_FACADE_DECODER', 'default')}: median of {args.reps} "
           f"{dt * 1e3:.1f} ms  {len(expect) / dt / 2**20:.1f} MiB/s "
           f"(best {len(expect) / ts[0] / 2**20:.1f}, worst {len(expect) / ts[-1] / 2**20:.1f})")
 
