@@ -31,6 +31,10 @@ package LZ4Ada.GPU is
 				Output_Length:  out    Interfaces.Integer_64;
 				Frame_Consumed: out    Interfaces.Integer_64);
 
+	-- lz4ada_rccl_version: the RCCL this process bound (22606 = 2.26.6).
+	function RCCL_Version return Interfaces.Integer_32;
+	pragma Import(C, RCCL_Version, "lz4ada_rccl_version");
+
 private
 
 	function C_Decode_Frame(Frame: System.Address; Len: Interfaces.Integer_64;

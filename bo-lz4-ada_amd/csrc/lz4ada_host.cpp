@@ -1694,8 +1694,7 @@ static bool try_reserve(DevBuf<T>& b, size_t count)
 // and a first-touch each time otherwise -- more than the decode itself on a
 // 1 GiB linked frame.  lz4ada_release_device_cache() frees them.  The
 // cache is never destroyed at thread exit (the HIP runtime may be gone).
-enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_TAB, SC_P, SC_F, SC_LONE, SC_U, SC_L,
-	                  SC_N };
+enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_TAB, SC_P, SC_F, SC_LONE, SC_U, SC_N };
 struct ScratchCache {
 	DevBuf<uint8_t> b[SC_N];
 };
@@ -2104,28 +2103,26 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		uint8_t* F = nullptr;
 		// sparse resolution (default): only history-derived bytes are jumped;
 		// LZ4ADA_LINKED_DENSE=1 keeps a word per output byte (round 2-3 form)
-		static const bool dense = getenv("LZ4ADA_LINKED_DENSE") != nullptr;
+		static const bool dense = [] {
+			const char* e = getenv("LZ4ADA_LINKED_DENSE");
+			return e && e[0] == '1';
+		}();
 		if (!dense) {
 			F = sink.dst(n);
 			struct {
 				uint8_t* p;
-			} d_U{ F ? scratch(SC_U, size_t((n + 63) / 32 * 4 + 64)) : nullptr },
-			    d_L{ d_U.p ? scratch(SC_L, size_t(std::max<int64_t>(n, 1)) * 4) : nullptr };
-			if (!d_L.p)
+			} d_U{ F ? scratch(SC_U, size_t(std::max<int64_t>(n, 1)) + 64) : nullptr };
+			if (!d_U.p)
 				return BULK_EXACT;
-			uint32_t* U = reinterpret_cast<uint32_t*>(d_U.p);
-			uint32_t* Lst = reinterpret_cast<uint32_t*>(d_L.p);
-			HIP_OK(hipMemsetAsync(U, 0, size_t((n + 63) / 32 * 4 + 64), stream));
-			HIP_OK(launch_link_init2(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, U, F,
-			                         Lst, d_ctr.p, stream));
+			HIP_OK(launch_link_init2(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, d_U.p, F,
+			                         d_ctr.p, stream));
 			d2h(ctr, d_ctr.p, sizeof ctr, stream);
 			phase("init2");
-			const int64_t nl = ctr[0];
 			for (int round = 0; ctr[0] > 0; ++round) {
 				if (round > 64)
 					return BULK_EXACT;  // never expected: every pointer goes strictly back
 				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
-				HIP_OK(launch_link_jump2(d_P.p, U, F, Lst, nl, d_tail[cur].p, tail_valid, d_ctr.p, stream));
+				HIP_OK(launch_link_jump2(d_P.p, d_U.p, F, n, d_tail[cur].p, tail_valid, d_ctr.p, stream));
 				d2h(ctr, d_ctr.p, sizeof ctr, stream);
 				if (ctr[1])
 					return BULK_EXACT;  // a reference before the frame start: the exact error
@@ -2342,7 +2339,7 @@ int lz4ada_launch_decode_variant(const void* d_frame, uint64_t frame_len,
                                  lz4ada_block_status* d_status, int variant, void* stream)
 {
 	return guarded(nullptr, [&] {
-		if (variant < 0 || variant > 6)
+		if (variant < 0 || variant > 8)
 			raise(LZ4ADA_ASSERTION_ERROR, "unknown decoder variant");
 		HIP_OK(launch_decode_variant(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
 		                             uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,

@@ -2547,16 +2547,26 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 	return hipGetLastError();
 }
 
-// The fused launch for independent blocks: two waves per block
-// (k_decode_idx2, mode 4) unless LZ4ADA_IDX_WAVES=1 picks k_decode_idx's
-// one wave (mode 3).
-int idx_fused_mode()
+// The fused launch for independent blocks.  One wave per block
+// (k_decode_idx, mode 3) while the blocks fill the chip's SIMDs twice;
+// two waves per block (k_decode_idx2, mode 4) for at most one block per
+// SIMD, where the second wave has a SIMD of its own (measured, DESIGN §4:
+// 1024 x 4 MiB mixed 12.05 -> 11.28 ms, but 2048 x 4 MiB 13.29 -> 13.98 ms:
+// each block's chain is latency-bound, so splitting a batch between two
+// waves shortens it little, and four waves per SIMD contend).
+// LZ4ADA_IDX_WAVES=1 / 2 forces one or the other.
+int idx_fused_mode(uint32_t nblocks)
 {
-	static const int mode = [] {
+	static const int forced = [] {
 		const char* e = getenv("LZ4ADA_IDX_WAVES");
-		return (e && e[0] == '1') ? 3 : 4;
+		return e ? (e[0] == '1' ? 3 : (e[0] == '2' ? 4 : 0)) : 0;
 	}();
-	return mode;
+	if (forced)
+		return forced;
+	int dev = 0, cus = 256;
+	if (hipGetDevice(&dev) == hipSuccess)
+		(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+	return nblocks <= uint32_t(4 * cus) ? 4 : 3;
 }
 
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
@@ -2570,7 +2580,7 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 	if (err != hipSuccess)
 		return err;
 	if (linked <= 0) {  // both passes in one launch (-1: one wave per block, -2: two)
-		const int mode = linked == -1 ? 3 : (linked == -2 ? 4 : idx_fused_mode());
+		const int mode = linked == -1 ? 3 : (linked == -2 ? 4 : idx_fused_mode(nblocks));
 		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
 		                            static_cast<const uint8_t*>(tab), d_out, d_status, mode, stream);
 	} else {

@@ -72,7 +72,7 @@ enum DecVariant : int { DEC_PC = 0, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4,
                         DEC_IDX_LINKED = 5, DEC_IDX_SPARSE = 6,
                         // the fused index decoder alone with one / two waves per block
                         DEC_IDX1_ALONE = 7, DEC_IDX2_ALONE = 8 };
-int idx_fused_mode();  // 3: k_decode_idx, 4: k_decode_idx2 (lz4ada_idx.hip)
+int idx_fused_mode(uint32_t nblocks);  // 3: k_decode_idx, 4: k_decode_idx2 (lz4ada_idx.hip)
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
@@ -171,16 +171,14 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h
                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
                             uint32_t* d_ctr, hipStream_t stream);
-// Sparse resolution: constants straight to F, pointer words, U bits and
-// list entries only for history-derived bytes; jumping over the list.
+// Sparse resolution: constants straight to F, pointer words and a 1 in
+// the byte map U only for history-derived bytes; jumping over those only.
 hipError_t launch_link_init2(const uint8_t* x, const uint8_t* y, const uint8_t* h,
                              const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                              const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                             uint32_t* d_U, uint8_t* d_F, uint32_t* d_L, uint32_t* d_ctr,
-                             hipStream_t stream);
-hipError_t launch_link_jump2(uint32_t* d_P, const uint32_t* d_U, uint8_t* d_F, const uint32_t* d_L,
-                             int64_t nl, const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_ctr,
-                             hipStream_t stream);
+                             uint8_t* d_U, uint8_t* d_F, uint32_t* d_ctr, hipStream_t stream);
+hipError_t launch_link_jump2(uint32_t* d_P, const uint8_t* d_U, uint8_t* d_F, int64_t n,
+                             const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_ctr, hipStream_t stream);
 hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
                             uint32_t* d_ctr, hipStream_t stream);
 hipError_t launch_link_emit(const uint32_t* d_P, int64_t n, uint8_t* d_F, hipStream_t stream);

@@ -1543,7 +1543,7 @@ hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
 	if (err == hipSuccess)
 		err = fuse ? launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
 		                                   static_cast<const uint8_t*>(tab), d_out, d_status,
-		                                   idx_fused_mode(), stream)
+		                                   idx_fused_mode(nblocks), stream)
 		           : launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab),
 		                          d_status, stream);
 	if (err == hipSuccess)

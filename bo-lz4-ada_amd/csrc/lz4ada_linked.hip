@@ -182,22 +182,23 @@ __global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int
 // pointer jumping (14% of the bench's mixed linked frame, 46% of dense:
 // the rest are literals, copied on inside the block).  k_link_init2 writes
 // every constant byte straight to its final place F, and for each
-// history-derived byte its pointer word P[a], bit a of U and an entry of
-// the list L; k_link_jump2 then runs over L only, reading a target's byte
-// from F when U says it is a constant and its word from P otherwise, and
-// writes F[a] when a word resolves -- no word per constant byte, no emit
-// pass.  U is read-only after init; P words change from a pointer to
-// another pointer along the same chain or to RES | byte, so a concurrent
-// reader sees a valid word either way (as in k_link_jump).
+// history-derived byte its pointer word P[a] and a 1 in the byte map U;
+// k_link_jump2 walks U 16 positions per lane and resolves only the marked
+// ones, reading a target's byte from F when U says it is a constant and its
+// word from P otherwise, and writes F[a] when a word resolves -- no word
+// per constant byte, no emit pass, no atomics.  U is read-only after init;
+// P words change from a pointer to another pointer along the same chain or
+// to RES | byte, so a concurrent reader sees a valid word either way (as in
+// k_link_jump).  (A compacted list with one global counter per wave was
+// 4x slower than the dense form: 4M atomics on one address.)
 __global__ __launch_bounds__(TPB) void k_link_init2(const uint8_t* __restrict__ x,
                                                     const uint8_t* __restrict__ y,
                                                     const uint8_t* __restrict__ h,
                                                     const lz4ada_block_desc* __restrict__ desc,
                                                     const lz4ada_block_status* __restrict__ st,
                                                     const int64_t* __restrict__ A, uint32_t nblocks,
-                                                    uint32_t* __restrict__ P, uint32_t* __restrict__ U,
-                                                    uint8_t* __restrict__ F, uint32_t* __restrict__ L,
-                                                    uint32_t* __restrict__ ctr)
+                                                    uint32_t* __restrict__ P, uint8_t* __restrict__ U,
+                                                    uint8_t* __restrict__ F, uint32_t* __restrict__ ctr)
 {
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
@@ -205,101 +206,99 @@ __global__ __launch_bounds__(TPB) void k_link_init2(const uint8_t* __restrict__ 
 	const uint64_t ob = desc[b].out_off;  // 256-byte aligned slot
 	const int64_t len = st[b].out_len;
 	const int64_t ab = A[b];
-	const uint32_t lane = lane_id();
-	// a wave covers 256 consecutive bytes of one block (4 per lane)
-	for (int64_t w0 = 256 * ((int64_t(blockIdx.y) * TPB + threadIdx.x) >> 6); w0 < len;
-	     w0 += 4 * int64_t(gridDim.y) * TPB) {
-		const int64_t q0 = w0 + 4 * lane;
-		uint32_t wx = 0, wy = 0, wh = 0;
-		if (q0 < len) {
-			wx = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(x) + ob + q0);
-			wy = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(y) + ob + q0);
-			wh = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(h) + ob + q0);
-		}
-		uint32_t fl = 0, fb = 0;  // history-derived bytes (bit i), constant bytes
-		uint32_t v[4];
+	uint32_t unres = 0;
+	for (int64_t q0 = 4 * (int64_t(blockIdx.y) * TPB + threadIdx.x); q0 < len;
+	     q0 += 4 * int64_t(gridDim.y) * TPB) {
+		const uint32_t wx = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(x) + ob + q0);
+		const uint32_t wy = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(y) + ob + q0);
+		const uint32_t wh = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(h) + ob + q0);
+		uint32_t fl = 0;  // byte i: 1 if history-derived
+		const int64_t a = ab + q0;
 #pragma unroll
 		for (int i = 0; i < 4; ++i) {
 			const uint32_t bx = (wx >> (8 * i)) & 255u, by = (wy >> (8 * i)) & 255u;
 			const uint32_t bh = (wh >> (8 * i)) & 255u;
-			const bool live = q0 + i < len;
-			const bool hist = live && bx != by;
-			v[i] = uint32_t(ab + int64_t(bx | (bh << 8)));
-			fl |= hist ? (1u << i) : 0u;
-			fb |= bx << (8 * i);
+			if (q0 + i < len && bx != by) {
+				fl |= 1u << (8 * i);
+				P[a + i] = uint32_t(ab + int64_t(bx | (bh << 8)));
+				++unres;
+			}
 		}
-		const int64_t a = ab + q0;  // batch-relative position of this lane's first byte
-		// the constant bytes to F (history-derived ones are written when resolved)
-		if (q0 < len) {
-			GLOBAL uint8_t* f = gptr(F) + a;
-			if (fl == 0 && q0 + 4 <= len && (a & 3) == 0) {
-				*reinterpret_cast<GLOBAL uint32_t*>(f) = fb;
+		GLOBAL uint8_t* f = gptr(F) + a;
+		GLOBAL uint8_t* u = gptr(U) + a;
+		if (q0 + 4 <= len && (a & 3) == 0) {
+			*reinterpret_cast<GLOBAL uint32_t*>(u) = fl;
+			if (fl == 0) {
+				*reinterpret_cast<GLOBAL uint32_t*>(f) = wx;
 			} else {
 #pragma unroll
 				for (int i = 0; i < 4; ++i)
-					if (q0 + i < len && !(fl >> i & 1u))
-						f[i] = uint8_t(fb >> (8 * i));
+					if (!(fl >> (8 * i) & 1u))
+						f[i] = uint8_t(wx >> (8 * i));
 			}
-		}
-		// pointer words and list entries of the history-derived bytes
-		const int32_t cnt = __popc(fl);
-		const int32_t inc = wave_incl_scan(cnt);
-		const int32_t tot = __shfl(inc, 63);
-		if (tot == 0)
-			continue;
-		uint32_t base = 0;
-		if (lane == 63)
-			base = atomicAdd(&ctr[0], uint32_t(tot));
-		base = __shfl(base, 63);
-		uint32_t e = base + uint32_t(inc - cnt);
+		} else {
 #pragma unroll
-		for (int i = 0; i < 4; ++i)
-			if (fl >> i & 1u) {
-				P[a + i] = v[i];
-				L[e++] = uint32_t(a + i);
-			}
-		// bits of U: this lane's 4 bits land in one or two 32-bit words
-		if (fl) {
-			const uint64_t bits = uint64_t(fl) << (a & 31);
-			const int64_t wi = a >> 5;
-			atomicOr(&U[wi], uint32_t(bits));
-			if (bits >> 32)
-				atomicOr(&U[wi + 1], uint32_t(bits >> 32));
+			for (int i = 0; i < 4; ++i)
+				if (q0 + i < len) {
+					u[i] = uint8_t(fl >> (8 * i));
+					if (!(fl >> (8 * i) & 1u))
+						f[i] = uint8_t(wx >> (8 * i));
+				}
 		}
 	}
+	wave_count(ctr, unres);
 }
 
-// One pointer-jumping round over the list L[0, nl).  ctr[0]: entries still
-// unresolved after the round; ctr[1]: references before the frame start.
-__global__ __launch_bounds__(TPB) void k_link_jump2(uint32_t* __restrict__ P, const uint32_t* __restrict__ U,
-                                                    uint8_t* __restrict__ F, const uint32_t* __restrict__ L,
-                                                    int64_t nl, const uint8_t* __restrict__ tail,
+// One pointer-jumping round over the marked positions of U[0, n).
+// ctr[0]: words still unresolved after the round; ctr[1]: references
+// before the frame start.
+__global__ __launch_bounds__(TPB) void k_link_jump2(uint32_t* __restrict__ P, const uint8_t* __restrict__ U,
+                                                    uint8_t* __restrict__ F, int64_t n,
+                                                    const uint8_t* __restrict__ tail,
                                                     int64_t tail_valid, uint32_t* __restrict__ ctr)
 {
 	uint32_t unres = 0, bad = 0;
-	for (int64_t j = int64_t(blockIdx.x) * TPB + threadIdx.x; j < nl; j += int64_t(gridDim.x) * TPB) {
-		const uint32_t a = L[j];
-		const uint32_t w = P[a];
-		if (w & RES)
-			continue;
-		const int64_t t = int64_t(w) - HISTORY_SIZE;
-		uint32_t f;
-		if (t < 0) {
-			if (t < -tail_valid) {
-				++bad;
-				continue;
-			}
-			f = RES | tail[HISTORY_SIZE + t];
-		} else if (!((U[t >> 5] >> (t & 31)) & 1u)) {
-			f = RES | F[t];  // a constant: final since k_link_init2
+	for (int64_t a0 = 16 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
+	     a0 += 16 * int64_t(gridDim.x) * TPB) {
+		u32x4 m;
+		if (a0 + 16 <= n) {
+			m = *reinterpret_cast<const GLOBAL u32x4*>(gptr(U) + a0);
 		} else {
-			f = P[t];  // resolved, or a pointer further back
+			uint32_t t[4] = { 0, 0, 0, 0 };
+			for (int64_t i = a0; i < n; ++i)
+				t[(i - a0) >> 2] |= uint32_t(U[i]) << (8 * ((i - a0) & 3));
+			m = u32x4{ t[0], t[1], t[2], t[3] };
 		}
-		P[a] = f;
-		if (f & RES)
-			F[a] = uint8_t(f);
-		else
-			++unres;
+		if ((m.x | m.y | m.z | m.w) == 0)
+			continue;
+		const uint32_t mw[4] = { m.x, m.y, m.z, m.w };
+#pragma unroll
+		for (int k = 0; k < 16; ++k) {
+			if (!((mw[k >> 2] >> (8 * (k & 3))) & 1u))
+				continue;
+			const int64_t a = a0 + k;
+			const uint32_t w = P[a];
+			if (w & RES)
+				continue;
+			const int64_t t = int64_t(w) - HISTORY_SIZE;
+			uint32_t f;
+			if (t < 0) {
+				if (t < -tail_valid) {
+					++bad;
+					continue;
+				}
+				f = RES | tail[HISTORY_SIZE + t];
+			} else if (!U[t]) {
+				f = RES | F[t];  // a constant: final since k_link_init2
+			} else {
+				f = P[t];  // resolved, or a pointer further back
+			}
+			P[a] = f;
+			if (f & RES)
+				F[a] = uint8_t(f);
+			else
+				++unres;
+		}
 	}
 	wave_count(&ctr[0], unres);
 	wave_count(&ctr[1], bad);
@@ -385,26 +384,24 @@ hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int
 hipError_t launch_link_init2(const uint8_t* x, const uint8_t* y, const uint8_t* h,
                              const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                              const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                             uint32_t* d_U, uint8_t* d_F, uint32_t* d_L, uint32_t* d_ctr,
-                             hipStream_t stream)
+                             uint8_t* d_U, uint8_t* d_F, uint32_t* d_ctr, hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
 	const int64_t per = 16 * 4 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
 	hipLaunchKernelGGL(link::k_link_init2, dim3(nblocks, gy), dim3(link::TPB), 0, stream, x, y, h, d_desc,
-	                   d_st, d_A, nblocks, d_P, d_U, d_F, d_L, d_ctr);
+	                   d_st, d_A, nblocks, d_P, d_U, d_F, d_ctr);
 	return hipGetLastError();
 }
 
-hipError_t launch_link_jump2(uint32_t* d_P, const uint32_t* d_U, uint8_t* d_F, const uint32_t* d_L,
-                             int64_t nl, const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_ctr,
-                             hipStream_t stream)
+hipError_t launch_link_jump2(uint32_t* d_P, const uint8_t* d_U, uint8_t* d_F, int64_t n,
+                             const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_ctr, hipStream_t stream)
 {
-	if (nl <= 0)
+	if (n <= 0)
 		return hipSuccess;
-	hipLaunchKernelGGL(link::k_link_jump2, dim3(grid_for(nl, 1)), dim3(link::TPB), 0, stream, d_P, d_U, d_F,
-	                   d_L, nl, d_tail, tail_valid, d_ctr);
+	hipLaunchKernelGGL(link::k_link_jump2, dim3(grid_for(n, 16)), dim3(link::TPB), 0, stream, d_P, d_U, d_F,
+	                   n, d_tail, tail_valid, d_ctr);
 	return hipGetLastError();
 }
 

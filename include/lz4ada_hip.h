@@ -250,6 +250,11 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
  * for the blocks pass 1 declines as sparse; no two-wave pass: blocks either
  * declines keep status code 10 (retry). */
 #define LZ4ADA_DECODE_IDX_SPARSE 6
+/* The fused index decoder alone with one wave per block (k_decode_idx) or
+ * two (k_decode_idx2, the default of LZ4ADA_DECODE_IDX / _ALONE unless
+ * LZ4ADA_IDX_WAVES=1); declined blocks keep status code 10. */
+#define LZ4ADA_DECODE_IDX1_ALONE 7
+#define LZ4ADA_DECODE_IDX2_ALONE 8
 int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                                  lz4ada_block_status *d_status, int variant, void *stream);
