@@ -788,11 +788,9 @@ struct lz4ada_decompressor {
 		const char* e = getenv("LZ4ADA_FACADE_DECODER");
 		if (e && !strcmp(e, "pc"))
 			return DEC_PC;
-		if (e && !strcmp(e, "wg"))
-			return DEC_WG;
 		if (e && !strcmp(e, "lone"))
 			return -2;  // the lone-block decoder at every size
-		return -1;  // lone (large blocks), else wg
+		return -1;  // lone (large blocks), else k_decode_pc
 	}
 
 	// Decompress_Full_Block through the bulk decoder for one block, into a
@@ -883,7 +881,7 @@ struct lz4ada_decompressor {
 		}
 		HIP_OK(hipMemcpyAsync(d_desc.p, &d, sizeof d, hipMemcpyHostToDevice, stream));
 		HIP_OK(launch_decode_variant(d_blk.p, uint64_t(std::max<int64_t>(blen, 1)), d_desc.p, 1,
-		                             d_scr.p, d_bst.p, fv < 0 ? int(DEC_WG) : fv, stream));
+		                             d_scr.p, d_bst.p, DEC_PC, stream));
 		return start;
 	}
 
@@ -2347,16 +2345,6 @@ int lz4ada_launch_decode_variant(const void* d_frame, uint64_t frame_len,
 	});
 }
 
-int lz4ada_launch_decode_wg(const void* d_frame, uint64_t frame_len,
-                            const lz4ada_block_desc* d_descs, int64_t nblocks, void* d_out,
-                            lz4ada_block_status* d_status, void* stream)
-{
-	return guarded(nullptr, [&] {
-		HIP_OK(launch_decode_wg(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
-		                        uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,
-		                        static_cast<hipStream_t>(stream)));
-	});
-}
 
 int64_t lz4ada_lone_scratch_bytes(int64_t n, int64_t cap) { return lone_scratch_bytes(n, cap); }
 

@@ -38,8 +38,13 @@
 namespace lz4ada {
 namespace idx {
 
+// Stored-block copies: nontemporal loads and stores (2; 1 = stores only,
+// 0 = neither).  A/B, 2048 x 4 MiB stored blocks, twice (tools/st_ab.sh,
+// DESIGN §3): 3.62 / 3.84 ms plain, 3.71 / 3.77 ms NT stores, 3.39 / 3.48 ms
+// NT loads and stores (with block checksums beside: 9.32 / 9.71, 9.49 /
+// 9.82, 8.68 / 8.73 ms).
 #ifndef LZ4ADA_STORED_NT
-#define LZ4ADA_STORED_NT 0
+#define LZ4ADA_STORED_NT 2
 #endif
 constexpr int SEG = 256;            // pass-1 segment per lane
 constexpr int CHUNK = 64 * SEG;     // pass-1 staged chunk (16 KiB)

@@ -68,7 +68,7 @@ struct SerialState {
 // All launch on `stream` and never synchronise.
 
 // Bulk independent-block decoders (LZ4ADA_DECODE_* in lz4ada_hip.h).
-enum DecVariant : int { DEC_PC = 0, DEC_WG = 2, DEC_IDX = 3, DEC_IDX_ALONE = 4,
+enum DecVariant : int { DEC_PC = 0, DEC_IDX = 3, DEC_IDX_ALONE = 4,
                         DEC_IDX_LINKED = 5, DEC_IDX_SPARSE = 6,
                         // the fused index decoder alone with one / two waves per block
                         DEC_IDX1_ALONE = 7, DEC_IDX2_ALONE = 8 };
@@ -86,12 +86,6 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                 uint8_t* d_out, lz4ada_block_status* d_status,
                                 hipStream_t stream);
-
-// Workgroup-per-block decoder alone (lz4ada_wg.hip); declined blocks get
-// status DS_RETRY.
-hipError_t launch_decode_wg(const uint8_t* d_frame, uint64_t frame_len,
-                            const lz4ada_block_desc* d_desc, uint32_t nblocks, uint8_t* d_out,
-                            lz4ada_block_status* d_status, hipStream_t stream);
 
 // Index-driven decoder alone (lz4ada_idx.hip): k_index + k_decode_idx;
 // declined blocks keep status DS_RETRY and are not decoded.  linked: the

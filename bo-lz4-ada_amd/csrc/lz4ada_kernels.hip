@@ -10,7 +10,7 @@
 //    sequences speculatively, consumer copies them); the bulk path's
 //    decoder for the blocks the index-driven decoder (lz4ada_idx.hip) and
 //    the literal-heavy decoder (lz4ada_sparse.hip) decline, and the lone
-//    facade block's fallback after the workgroup decoder (lz4ada_wg.hip).
+//    facade's small blocks.
 //    Long or unusual tokens (multi-byte length extensions, anything
 //    malformed) go through a wave-cooperative one-token path that also
 //    produces the precise error.
@@ -1417,18 +1417,9 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 		                   d_desc, nblocks, d_out, d_status, 1, 0);
 		return hipGetLastError();
 	}
-	if (variant == DEC_WG) {
-		const hipError_t err = launch_decode_wg(d_frame, frame_len, d_desc, nblocks, d_out,
-		                                        d_status, stream);
-		if (err != hipSuccess)
-			return err;
-	}
-	if (variant != DEC_WG)
-		return hipErrorInvalidValue;  // 1 was the round-1 one-wave decoder (retired)
-	// the blocks the workgroup decoder declined
-	hipLaunchKernelGGL(k_decode_pc, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
-	                   d_desc, nblocks, d_out, d_status, 1, 0);
-	return hipGetLastError();
+	// 1 (the round-1 one-wave decoder) and 2 (the workgroup decoder, retired
+	// in round 4: no faster than k_decode_pc on the facade's small blocks)
+	return hipErrorInvalidValue;
 }
 
 hipError_t launch_decode_pc(const uint8_t* d_frame, uint64_t frame_len,
@@ -1457,12 +1448,10 @@ hipError_t launch_decode_blocks(const uint8_t* d_frame, uint64_t frame_len,
 static int decoder_variant()
 {
 	// Default: the index-driven decoder (lz4ada_idx.hip), the two-wave
-	// decoder for the blocks it declines.  LZ4ADA_DECODER=pc / wg select
-	// the two-wave or the workgroup decoder.
+	// decoder for the blocks it declines.  LZ4ADA_DECODER=pc selects the
+	// two-wave decoder alone.
 	static const int variant = [] {
 		const char* e = getenv("LZ4ADA_DECODER");
-		if (e && e[0] == 'w' && e[1] == 'g')
-			return int(DEC_WG);
 		if (e && e[0] == 'p')
 			return int(DEC_PC);
 		return int(DEC_IDX);

@@ -203,7 +203,6 @@ _sig = {
     "lz4ada_launch_decode": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lz4ada_launch_decode_variant": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, ctypes.c_int, _vp],
                                      ctypes.c_int),
-    "lz4ada_launch_decode_wg": ([_vp, ctypes.c_uint64, _vp, _i64, _vp, _vp, _vp], ctypes.c_int),
     "lz4ada_launch_block_checksums": ([_vp, _vp, _i64, _vp, _vp], ctypes.c_int),
     "lz4ada_output_checksums_device": ([_vp, _vp, _vp, _i64, _vp, _vp], ctypes.c_int),
     "lz4ada_decode_frame": ([_vp, _i64, _vp, _i64, _pi64, _pi64], ctypes.c_int),
@@ -549,7 +548,7 @@ def launch_decode(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=
                                      stream), _thread_error())
 
 
-DECODE_PC, DECODE_WG, DECODE_IDX, DECODE_IDX_ALONE, DECODE_IDX_LINKED = 0, 2, 3, 4, 5
+DECODE_PC, DECODE_IDX, DECODE_IDX_ALONE, DECODE_IDX_LINKED = 0, 3, 4, 5
 DECODE_IDX_SPARSE = 6
 DECODE_IDX1_ALONE, DECODE_IDX2_ALONE = 7, 8  # fused index decoder alone: one / two waves per block
 
@@ -557,15 +556,9 @@ DECODE_IDX1_ALONE, DECODE_IDX2_ALONE = 7, 8  # fused index decoder alone: one / 
 def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,
                           stream=0):
     """One of the bulk decoders: DECODE_IDX (default: index-driven + two-wave
-    retry), DECODE_PC, DECODE_WG, DECODE_IDX_ALONE."""
+    retry), DECODE_PC, DECODE_IDX_ALONE."""
     _check(_lib.lz4ada_launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out,
                                              d_status, variant, stream), _thread_error())
-
-
-def launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status, stream=0):
-    """Workgroup-per-block decoder alone; declined blocks keep status DS_RETRY."""
-    _check(_lib.lz4ada_launch_decode_wg(d_frame, frame_len, d_descs, nblocks, d_out, d_status,
-                                        stream), _thread_error())
 
 
 def lone_scratch_bytes(n: int, cap: int) -> int:

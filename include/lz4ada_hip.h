@@ -231,11 +231,9 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
                          const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                          lz4ada_block_status *d_status, void *stream);
 /* Decoder variants of the bulk path: the two-wave
- * producer/consumer decoder, and the workgroup decoder followed by the
- * two-wave decoder for declined blocks (1, the round-1 one-wave decoder, is
- * retired: LZ4ADA_DEVICE_ERROR). */
+ * producer/consumer decoder (1, the round-1 one-wave decoder, and 2, the
+ * workgroup decoder, are retired: LZ4ADA_DEVICE_ERROR). */
 #define LZ4ADA_DECODE_PC 0
-#define LZ4ADA_DECODE_WG 2
 /* Index-driven two-pass decoder (k_index + k_decode_idx, lz4ada_idx.hip),
  * then the two-wave decoder for the blocks it declines; _ALONE skips that
  * second step (declined blocks keep status code 10). */
@@ -272,12 +270,6 @@ int lz4ada_launch_decode_lone(const void *d_blk, int64_t n, void *d_out, int64_t
                               lz4ada_block_status *d_status, void *d_scratch,
                               int64_t scratch_bytes, void *stream);
 
-/* The workgroup-per-block decoder alone: blocks it declines (malformed
- * data, oversize sequences) keep status code 10 (retry) and are not
- * decoded; lz4ada_launch_decode runs it and then redoes those blocks. */
-int lz4ada_launch_decode_wg(const void *d_frame, uint64_t frame_len,
-                            const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
-                            lz4ada_block_status *d_status, void *stream);
 int lz4ada_launch_block_checksums(const void *d_frame, const lz4ada_block_desc *d_descs,
                                   int64_t nblocks, lz4ada_block_status *d_status,
                                   void *stream);

@@ -276,7 +276,7 @@ def test_device_resident_blocks():
 
 # ------------------------------------------- bench-sized blocks (regression)
 
-@pytest.mark.parametrize("variant", ["pc", "wg", "idx", "idx1"])
+@pytest.mark.parametrize("variant", ["pc", "idx", "idx1"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
 def test_bench_blocks_exact(kind, variant):
     """The bench's own unique 4 MiB blocks (seed 0x4C5A3441 + i) decode
@@ -296,8 +296,8 @@ def test_bench_blocks_exact(kind, variant):
     d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
     sh = torch.cuda.current_stream().cuda_stream
     lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), nb, d_st.data_ptr(), sh)
-    v = {"pc": lz4ada.DECODE_PC, "wg": lz4ada.DECODE_WG,
-         "idx": lz4ada.DECODE_IDX, "idx1": lz4ada.DECODE_IDX1_ALONE}[variant]
+    v = {"pc": lz4ada.DECODE_PC, "idx": lz4ada.DECODE_IDX,
+         "idx1": lz4ada.DECODE_IDX1_ALONE}[variant]
     lz4ada.launch_decode_variant(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
                                  d_out.data_ptr(), d_st.data_ptr(), v, sh)
     torch.cuda.synchronize()
@@ -336,68 +336,6 @@ def test_sharded_decode_each_rank_share(world):
         for j, ln in enumerate(lens):
             got += host[j * 256 * 1024:j * 256 * 1024 + ln]
     assert got == expected
-
-
-def _run_wg_alone(frame):
-    """Decode a frame's blocks with the workgroup decoder only; returns
-    (descs, statuses, output bytes)."""
-    import torch
-    info, descs = lz4ada.frame_index(frame)
-    nb = info.nblocks
-    bmax = info.block_max
-    dev = torch.device("cuda:0")
-    d_frame = torch.frombuffer(bytearray(frame), dtype=torch.uint8).to(dev)
-    d_desc = torch.frombuffer(bytearray(bytes(descs)[:nb * 32]), dtype=torch.uint8).to(dev)
-    d_out = torch.zeros(nb * bmax, dtype=torch.uint8, device=dev)
-    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
-    lz4ada.launch_decode_wg(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
-                            d_out.data_ptr(), d_st.data_ptr(),
-                            torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    st = (lz4ada.BlockStatus * nb).from_buffer_copy(d_st.cpu().numpy().tobytes())
-    return descs, st, d_out.cpu().numpy().tobytes()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "rle"])
-@pytest.mark.parametrize("bmax", [64 << 10, 4 << 20])
-def test_wg_decoder_alone(kind, bmax):
-    """The workgroup decoder on its own: exact output for every block it
-    accepts, and it accepts every block of the non-RLE classes."""
-    blocks = [lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 0x4C5A3441 + i, bmax) for i in range(6)]
-    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax)
-    descs, st, out = _run_wg_alone(frame)
-    bad, retried = [], 0
-    for i, (c, r) in enumerate(blocks):
-        if st[i].code == lz4ada.DS_RETRY:
-            retried += 1
-            continue
-        got = out[i * bmax:i * bmax + len(r)]
-        if st[i].code or st[i].out_len != len(r) or got != r:
-            j = next((k for k in range(min(len(r), len(got))) if got[k] != r[k]), -1)
-            bad.append((i, st[i].code, st[i].out_len, len(r), j))
-    assert not bad, bad
-    if kind != "rle":
-        assert retried == 0
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246"])
-def test_wg_decoder_alone_on_vectors(name, digests):
-    """Reference vectors' blocks through the workgroup decoder alone: every
-    accepted block is byte-exact (whole-frame digest when all are accepted)."""
-    frame = read_vector(name, "lz4")
-    descs, st, out = _run_wg_alone(frame)
-    info, _ = lz4ada.frame_index(frame)
-    pieces, all_ok = [], True
-    for i in range(info.nblocks):
-        if st[i].code != 0:
-            assert st[i].code == lz4ada.DS_RETRY, st[i].code
-            all_ok = False
-            continue
-        pieces.append(out[i * info.block_max:i * info.block_max + st[i].out_len])
-    if all_ok and info.independent:
-        assert hashlib.sha256(b"".join(pieces)).hexdigest() == digests[name]["sha256"]
 
 
 def _run_variant_alone(frame, variant):

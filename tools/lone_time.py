@@ -35,12 +35,12 @@ def main():
             lz4ada.launch_decode_lone(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_st.data_ptr(),
                                       d_sc.data_ptr(), sb, stream.cuda_stream)
 
-        def wg():
-            lz4ada.launch_decode_wg(d_in.data_ptr(), n, d_desc.data_ptr(), 1, d_out.data_ptr(),
-                                    d_st.data_ptr(), stream.cuda_stream)
+        def pc():
+            lz4ada.launch_decode_variant(d_in.data_ptr(), n, d_desc.data_ptr(), 1, d_out.data_ptr(),
+                                         d_st.data_ptr(), lz4ada.DECODE_PC, stream.cuda_stream)
 
         res = {}
-        for name, fn in (("lone", lone), ("wg", wg)):
+        for name, fn in (("lone", lone), ("pc", pc)):
             fn()
             torch.cuda.synchronize()
             st = lz4ada.BlockStatus.from_buffer_copy(d_st.cpu().numpy().tobytes())

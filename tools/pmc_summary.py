@@ -26,7 +26,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import kernel_src_hash  # noqa: E402
-KERNELS = ("k_decode_idx", "k_index", "k_decode_sparse", "k_decode_pc", "k_decode_wg", "k_decode_blocks",
+KERNELS = ("k_decode_idx", "k_index", "k_decode_sparse", "k_decode_pc", "k_decode_blocks",
            "k_xxh32_rows", "k_serial_block", "k_xxh32_update",
            "k_compact")
 

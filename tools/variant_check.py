@@ -19,7 +19,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import lz4ada  # noqa: E402
 
-VARIANTS = {"pc": lz4ada.DECODE_PC, "wg": lz4ada.DECODE_WG,
+VARIANTS = {"pc": lz4ada.DECODE_PC,
             "idx": lz4ada.DECODE_IDX, "idx_alone": lz4ada.DECODE_IDX_ALONE}
 
 
