@@ -249,53 +249,62 @@ __global__ __launch_bounds__(TPB) void k_link_init2(const uint8_t* __restrict__ 
 	wave_count(ctr, unres);
 }
 
-// One pointer-jumping round over the marked positions of U[0, n).
-// ctr[0]: words still unresolved after the round; ctr[1]: references
-// before the frame start.
+// One pointer-jumping round over the marked positions of U[0, n), four
+// positions per lane: the marks and words of all four, then every target's
+// mark, byte and word, are loaded together before any is used (one
+// dependent round trip per level, not one per position).  ctr[0]: words
+// still unresolved after the round; ctr[1]: references before the frame
+// start.
 __global__ __launch_bounds__(TPB) void k_link_jump2(uint32_t* __restrict__ P, const uint8_t* __restrict__ U,
                                                     uint8_t* __restrict__ F, int64_t n,
                                                     const uint8_t* __restrict__ tail,
                                                     int64_t tail_valid, uint32_t* __restrict__ ctr)
 {
 	uint32_t unres = 0, bad = 0;
-	for (int64_t a0 = 16 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
-	     a0 += 16 * int64_t(gridDim.x) * TPB) {
-		u32x4 m;
-		if (a0 + 16 <= n) {
-			m = *reinterpret_cast<const GLOBAL u32x4*>(gptr(U) + a0);
+	GLOBAL uint32_t* Pg = gptr(P);
+	for (int64_t a0 = 4 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
+	     a0 += 4 * int64_t(gridDim.x) * TPB) {
+		uint32_t um;
+		if (a0 + 4 <= n) {
+			um = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(U) + a0);
 		} else {
-			uint32_t t[4] = { 0, 0, 0, 0 };
+			um = 0;
 			for (int64_t i = a0; i < n; ++i)
-				t[(i - a0) >> 2] |= uint32_t(U[i]) << (8 * ((i - a0) & 3));
-			m = u32x4{ t[0], t[1], t[2], t[3] };
+				um |= uint32_t(U[i]) << (8 * (i - a0));
 		}
-		if ((m.x | m.y | m.z | m.w) == 0)
+		if (um == 0)
 			continue;
-		const uint32_t mw[4] = { m.x, m.y, m.z, m.w };
+		uint32_t w[4];
 #pragma unroll
-		for (int k = 0; k < 16; ++k) {
-			if (!((mw[k >> 2] >> (8 * (k & 3))) & 1u))
+		for (int i = 0; i < 4; ++i)
+			w[i] = (um >> (8 * i) & 1u) ? Pg[a0 + i] : RES;
+		int64_t t[4];
+		uint32_t tu[4], tf[4], tp[4];
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			t[i] = (w[i] & RES) ? 0 : int64_t(w[i]) - HISTORY_SIZE;
+			const int64_t tc = t[i] < 0 ? 0 : t[i];
+			tu[i] = (w[i] & RES) || t[i] < 0 ? 0u : uint32_t(U[tc]);
+			tf[i] = (w[i] & RES) || t[i] < 0 ? 0u : uint32_t(F[tc]);
+			tp[i] = (w[i] & RES) || t[i] < 0 ? RES : Pg[tc];
+		}
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			if (w[i] & RES)
 				continue;
-			const int64_t a = a0 + k;
-			const uint32_t w = P[a];
-			if (w & RES)
-				continue;
-			const int64_t t = int64_t(w) - HISTORY_SIZE;
 			uint32_t f;
-			if (t < 0) {
-				if (t < -tail_valid) {
+			if (t[i] < 0) {
+				if (t[i] < -tail_valid) {
 					++bad;
 					continue;
 				}
-				f = RES | tail[HISTORY_SIZE + t];
-			} else if (!U[t]) {
-				f = RES | F[t];  // a constant: final since k_link_init2
+				f = RES | tail[HISTORY_SIZE + t[i]];
 			} else {
-				f = P[t];  // resolved, or a pointer further back
+				f = tu[i] ? tp[i] : (RES | tf[i]);  // a constant is final since k_link_init2
 			}
-			P[a] = f;
+			Pg[a0 + i] = f;
 			if (f & RES)
-				F[a] = uint8_t(f);
+				F[a0 + i] = uint8_t(f);
 			else
 				++unres;
 		}
@@ -400,7 +409,7 @@ hipError_t launch_link_jump2(uint32_t* d_P, const uint8_t* d_U, uint8_t* d_F, in
 {
 	if (n <= 0)
 		return hipSuccess;
-	hipLaunchKernelGGL(link::k_link_jump2, dim3(grid_for(n, 16)), dim3(link::TPB), 0, stream, d_P, d_U, d_F,
+	hipLaunchKernelGGL(link::k_link_jump2, dim3(grid_for(n, 4)), dim3(link::TPB), 0, stream, d_P, d_U, d_F,
 	                   n, d_tail, tail_valid, d_ctr);
 	return hipGetLastError();
 }

@@ -53,7 +53,7 @@ def main():
             torch.cuda.synchronize()
             res[name] = (e0.elapsed_time(e1) / args.reps, ok, st.code)
         print(f"{kind:8s} {args.size >> 10} KiB (comp {n}): lone {res['lone'][0]:.3f} ms "
-              f"ok={res['lone'][1]}  wg {res['wg'][0]:.3f} ms ok={res['wg'][1]}", flush=True)
+              f"ok={res['lone'][1]}  pc {res['pc'][0]:.3f} ms ok={res['pc'][1]}", flush=True)
 
 
 if __name__ == "__main__":
