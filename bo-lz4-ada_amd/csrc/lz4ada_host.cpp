@@ -2099,11 +2099,13 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
 		uint32_t ctr[2] = { 0, 0 };
 		uint8_t* F = nullptr;
-		// sparse resolution (default): only history-derived bytes are jumped;
-		// LZ4ADA_LINKED_DENSE=1 keeps a word per output byte (round 2-3 form)
+		// dense resolution: a word per output byte (default); sparse: only the
+		// history-derived bytes are jumped
+		// (sparse, LZ4ADA_LINKED_SPARSE=1: measured slower -- three gathers per
+		// target instead of one word -- DESIGN §7)
 		static const bool dense = [] {
-			const char* e = getenv("LZ4ADA_LINKED_DENSE");
-			return e && e[0] == '1';
+			const char* e = getenv("LZ4ADA_LINKED_SPARSE");
+			return !(e && e[0] == '1');
 		}();
 		if (!dense) {
 			F = sink.dst(n);

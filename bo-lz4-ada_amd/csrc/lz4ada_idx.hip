@@ -38,8 +38,9 @@
 namespace lz4ada {
 namespace idx {
 
-// Stored-block copies: nontemporal loads and stores (2; 1 = stores only,
-// 0 = neither).  A/B, 2048 x 4 MiB stored blocks, twice (tools/st_ab.sh,
+// Stored-block copies without a block checksum: nontemporal loads and
+// stores (2; 1 = stores only, 0 = neither).  With a block checksum the copy
+// stays cached: the checksum kernel beside it reads the same payload.  A/B, 2048 x 4 MiB stored blocks, twice (tools/st_ab.sh,
 // DESIGN §3): 3.62 / 3.84 ms plain, 3.71 / 3.77 ms NT stores, 3.39 / 3.48 ms
 // NT loads and stores (with block checksums beside: 9.32 / 9.71, 9.49 /
 // 9.82, 8.68 / 8.73 ms).
@@ -1322,7 +1323,12 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			Src S0;
 			S0.in = in;
 			S0.lim = lim;
-			wave_literal<LZ4ADA_STORED_NT>(ob, 0, S0, 0, n);
+			// nontemporal copy unless the block checksum kernel beside this
+			// one reads the same payload (it then finds it in the caches)
+			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM)
+				wave_literal<0>(ob, 0, S0, 0, n);
+			else
+				wave_literal<LZ4ADA_STORED_NT>(ob, 0, S0, 0, n);
 		}
 		if (lane == 0) {
 			status[b].code = code;
@@ -2152,10 +2158,11 @@ __device__ __forceinline__ void decode_block2(DecLds2& L, const uint8_t* __restr
 			S0.in = in;
 			S0.lim = lim;
 			const int32_t mid = (n >> 1) & ~1023;
-			if (w == 0)
-				wave_literal<LZ4ADA_STORED_NT>(ob, 0, S0, 0, mid);
+			const int32_t c0 = w == 0 ? 0 : mid, c1 = w == 0 ? mid : n;
+			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM)
+				wave_literal<0>(ob, c0, S0, c0, c1 - c0);
 			else
-				wave_literal<LZ4ADA_STORED_NT>(ob, mid, S0, mid, n - mid);
+				wave_literal<LZ4ADA_STORED_NT>(ob, c0, S0, c0, c1 - c0);
 		}
 		if (tid == 0) {
 			status[b].code = code;
