@@ -12,7 +12,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <future>
+#include <mutex>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -123,6 +126,88 @@ struct DevBuf {
 		release();
 		HIP_OK(hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T) + 64));
 		n = count;
+	}
+};
+
+// Pinned host memory, grow-only (the facade's output staging).
+struct PinBuf {
+	uint8_t* p = nullptr;
+	size_t n = 0;
+	PinBuf() = default;
+	PinBuf(const PinBuf&) = delete;
+	PinBuf& operator=(const PinBuf&) = delete;
+	~PinBuf()
+	{
+		if (p)
+			(void)hipHostFree(p);
+	}
+	void reserve(size_t count)
+	{
+		if (count <= n && p)
+			return;
+		if (p)
+			(void)hipHostFree(p);
+		p = nullptr;
+		n = 0;
+		HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1), hipHostMallocDefault));
+		n = count;
+	}
+};
+
+// One long-lived helper thread running one job at a time (the facade's
+// content checksum of a large block while the caller feeds the next one);
+// wait() joins the current job.
+struct Worker {
+	std::thread th;
+	std::mutex mu;
+	std::condition_variable cv, done_cv;
+	std::function<void()> job;
+	bool busy = false, stop = false;
+	Worker() = default;
+	Worker(const Worker&) = delete;
+	Worker& operator=(const Worker&) = delete;
+	~Worker()
+	{
+		{
+			std::lock_guard<std::mutex> l(mu);
+			stop = true;
+		}
+		cv.notify_one();
+		if (th.joinable())
+			th.join();
+	}
+	void submit(std::function<void()> f)
+	{
+		wait();
+		if (!th.joinable())
+			th = std::thread([this] { loop(); });
+		{
+			std::lock_guard<std::mutex> l(mu);
+			job = std::move(f);
+			busy = true;
+		}
+		cv.notify_one();
+	}
+	void wait()
+	{
+		std::unique_lock<std::mutex> l(mu);
+		done_cv.wait(l, [this] { return !busy; });
+	}
+	void loop()
+	{
+		std::unique_lock<std::mutex> l(mu);
+		for (;;) {
+			cv.wait(l, [this] { return (busy && job) || stop; });
+			if (!(busy && job))
+				return;  // stop, nothing pending
+			std::function<void()> f = std::move(job);
+			job = nullptr;
+			l.unlock();
+			f();
+			l.lock();
+			busy = false;
+			done_cv.notify_all();
+		}
 	}
 };
 
@@ -453,14 +538,13 @@ struct lz4ada_decompressor {
 	DevBuf<uint8_t> d_blk;
 	lz4ada_xxh32_state hash_all{};  // Hash_All_Data, over the bytes the GPU decoded
 	// A large block's content hash runs on a helper thread while the caller
-	// feeds the next block (the caller's Buffer is not modified between
-	// calls); every reader of hash_all joins it first.
-	std::future<void> hash_job;
-	void hash_wait()
-	{
-		if (hash_job.valid())
-			hash_job.get();
-	}
+	// feeds the next block, over the pinned staging copy of its output (our
+	// memory, so the caller may reuse its Buffer); every reader of hash_all
+	// or writer of the staging joins it first.
+	Worker hasher;
+	void hash_wait() { hasher.wait(); }
+	PinBuf stage;  // a block's output on its way to the caller's Buffer
+	PinBuf stage_st;  // its status
 	std::vector<uint8_t> blk_tmp;  // a block assembled from cached + new input
 	DevBuf<lz4ada_xxh32_state> d_tmp_hash;
 	DevBuf<SerialState> d_serial;
@@ -494,8 +578,7 @@ struct lz4ada_decompressor {
 	lz4ada_decompressor() { lz4ada_xxh32_reset(&hash_all, 0); }
 	~lz4ada_decompressor()
 	{
-		if (hash_job.valid())
-			hash_job.wait();
+		hash_wait();
 		if (side) {
 			(void)hipStreamSynchronize(side);
 			(void)hipStreamDestroy(side);
@@ -689,15 +772,7 @@ struct lz4ada_decompressor {
 		// into a scratch slot; the mirror takes the output only once the
 		// checksum has passed.  A block known to fail (the bulk path stopped
 		// at it) is checked before anything is launched.
-		auto check = [&] {
-			lz4ada_xxh32_state h;
-			lz4ada_xxh32_reset(&h, 0);
-			host_xxh32_update(h, blk, size_t(raw_len));
-			const uint32_t got = host_xxh32_final(h);
-			const uint32_t expect = load32(blk + blen - bcl);
-			return std::make_pair(got == expect, "Declared checksum is 0x" + hex32(expect) +
-			                                             ", but computed one is 0x" + hex32(got) + ".");
-		};
+		auto check = [&] { return block_checksum(blk, blen); };
 		if (checksum_first && bcl > 0) {
 			checksum_first = false;
 			const auto c = check();
@@ -707,8 +782,12 @@ struct lz4ada_decompressor {
 		if (blen > 0)
 			HIP_OK(hipMemcpyAsync(d_blk.p, blk, size_t(blen), hipMemcpyHostToDevice, stream));
 		phase("h2d");
-		const int64_t fast_start = launch_fast_block(raw_len, blen, buflen);
-		if (bcl > 0) {
+		const LoneResult lr = lone_block(blk, blen, buf, buflen, first, last);
+		phase("lone");
+		if (lr == LONE_DONE)
+			return;
+		const int64_t fast_start = lr == LONE_DECLINED ? -1 : launch_fast_block(raw_len, blen, buflen);
+		if (bcl > 0 && lr != LONE_DECLINED) {
 			const auto c = check();
 			phase("cksum");
 			if (!c.first) {
@@ -756,19 +835,12 @@ struct lz4ada_decompressor {
 			return;
 		static const bool trace = getenv("LZ4ADA_TRACE_FACADE") != nullptr;
 		const auto t0 = std::chrono::steady_clock::now();
-		hash_wait();  // the previous block's bytes may share this Buffer range
-		HIP_OK(hipMemcpyAsync(buf + first, d_buf.p + first, size_t(nout), hipMemcpyDeviceToHost,
-		                      stream));
+		hash_wait();  // the staging may still be hashed
+		stage.reserve(size_t(nout));
+		HIP_OK(hipMemcpyAsync(stage.p, d_buf.p + first, size_t(nout), hipMemcpyDeviceToHost, stream));
 		HIP_OK(hipStreamSynchronize(stream));
 		const auto t1 = std::chrono::steady_clock::now();
-		if (m.content_checksum_length != 0) {
-			const uint8_t* p = buf + first;
-			if (nout >= (int64_t(256) << 10))
-				hash_job = std::async(std::launch::async,
-				                      [this, p, nout] { host_xxh32_update(hash_all, p, size_t(nout)); });
-			else
-				host_xxh32_update(hash_all, p, size_t(nout));
-		}
+		to_caller(buf + first, nout);
 		if (trace)
 			fprintf(stderr, "[facade]   d2h %.3f ms, content hash %.3f ms\n",
 			        std::chrono::duration<double, std::milli>(t1 - t0).count(),
@@ -776,13 +848,28 @@ struct lz4ada_decompressor {
 			                .count());
 	}
 
+	// The staged output (stage.p, nout bytes) to the caller's Buffer and into
+	// the content checksum -- on the helper thread for a large block.
+	void to_caller(uint8_t* dst, int64_t nout)
+	{
+		memcpy(dst, stage.p, size_t(nout));
+		if (m.content_checksum_length == 0)
+			return;
+		const uint8_t* p = stage.p;
+		if (nout >= (int64_t(64) << 10))
+			hasher.submit([this, p, nout] { host_xxh32_update(hash_all, p, size_t(nout)); });
+		else
+			host_xxh32_update(hash_all, p, size_t(nout));
+	}
+
 	// A lone block is latency-bound: the lone-block decoder (every step
-	// parallel over the block's bytes, lz4ada_lone.hip) decodes a 4 MiB
-	// block ~25x sooner than the 512-lane workgroup decoder, which in turn
-	// beats the two-wave one (tools/lone_time.py, tools/facade_time.py).
-	// Below LONE_MIN compressed bytes the workgroup decoder's single launch
-	// wins.  LZ4ADA_FACADE_DECODER=wg / pc picks the others.
-	static constexpr int64_t LONE_MIN = 16 << 10;
+	// parallel over the block's bytes, lz4ada_lone.hip) decodes a 4 MiB mixed
+	// block in ~0.2 ms against ~21 ms for k_decode_pc's one workgroup
+	// (tools/lone_time.py).  Below LONE_MIN compressed bytes k_decode_pc's
+	// single launch wins (16 KiB mixed blocks, 8 KB compressed: lone 0.051 ms,
+	// pc 0.090; pc's time grows with the block, lone's ~0.045 ms floor is its
+	// five launches).  LZ4ADA_FACADE_DECODER=pc / lone forces one.
+	static constexpr int64_t LONE_MIN = 6 << 10;
 	static int facade_variant()
 	{
 		const char* e = getenv("LZ4ADA_FACADE_DECODER");
@@ -838,6 +925,97 @@ struct lz4ada_decompressor {
 		return output_pos_history >= HISTORY_SIZE && output_pos_history <= HISTORY_SIZE + 6;
 	}
 
+	std::pair<bool, std::string> block_checksum(const uint8_t* blk, int64_t blen) const
+	{
+		const int bcl = m.block_checksum_length;
+		lz4ada_xxh32_state h;
+		lz4ada_xxh32_reset(&h, 0);
+		host_xxh32_update(h, blk, size_t(blen - bcl));
+		const uint32_t got = host_xxh32_final(h);
+		const uint32_t expect = load32(blk + blen - bcl);
+		return std::make_pair(got == expect, "Declared checksum is 0x" + hex32(expect) +
+		                                             ", but computed one is 0x" + hex32(got) + ".");
+	}
+
+	// A compressed block for the lone-block decoder: every block of a linked
+	// frame (the reference's history as readable words in front of its
+	// output), an independent frame's from LONE_MIN compressed bytes.  Its
+	// two halves run around the host checksum (Check_Checksum before any
+	// output, :672-676), and the emit writes straight into the mirror at the
+	// reference's Output_Pos -- only when the block decoded cleanly, so a
+	// decline (a reference past the history, D1 risk, a content-size or
+	// slot overrun, anything the reference would reject) leaves the mirror
+	// untouched for the exact path.  The status and the output come back in
+	// one round trip through pinned staging.
+	enum LoneResult { LONE_NOT_TAKEN, LONE_DONE, LONE_DECLINED };
+	LoneResult lone_block(const uint8_t* blk, int64_t blen, uint8_t* buf, int64_t buflen, int64_t& first,
+	                      int64_t& last)
+	{
+		const int bcl = m.block_checksum_length;
+		const int64_t raw_len = blen - bcl;
+		if (!m.is_compressed || raw_len <= 0 || raw_len > INT32_MAX || getenv("LZ4ADA_FACADE_EXACT"))
+			return LONE_NOT_TAKEN;
+		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
+		const int fv = facade_variant();
+		if (!linked && !(fv < 0 && (raw_len >= LONE_MIN || fv == -2)))
+			return LONE_NOT_TAKEN;
+		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;  // :678-680
+		if (buflen - start <= 0)
+			return LONE_NOT_TAKEN;
+		int64_t cap = block_room(buflen - start, raw_len, true);
+		if (m.has_content_size)  // more output: the exact path raises mid-block, as the reference does
+			cap = int64_t(std::min<uint64_t>(uint64_t(cap), m.size_remaining));
+		if (cap <= 0 || cap > (int64_t(1) << 30))
+			return LONE_NOT_TAKEN;
+		int64_t n0 = 0, n1 = 0;
+		if (linked)
+			history_of(start, n0, n1);
+		const int64_t sb = lone_scratch_bytes(raw_len, cap);
+		d_lone.reserve(size_t(sb));
+		HIP_OK(launch_decode_lone_parse(d_blk.p, raw_len, cap, d_bst.p, d_lone.p, sb, stream,
+		                                linked ? d_buf.p + output_pos_history - n0 : nullptr, int32_t(n0),
+		                                linked ? d_buf.p : nullptr, int32_t(n1),
+		                                linked && d1_window() ? 1 : 0));
+		if (bcl > 0) {
+			const auto c = block_checksum(blk, blen);
+			if (!c.first) {
+				HIP_OK(hipStreamSynchronize(stream));
+				raise(LZ4ADA_CHECKSUM_ERROR, c.second);
+			}
+		}
+		HIP_OK(launch_decode_lone_emit(raw_len, d_buf.p + start, cap, d_bst.p, d_lone.p, stream,
+		                               int32_t(n0 + n1)));
+		// the likely share of the output comes back with the status
+		const int64_t spec = std::min<int64_t>(cap, std::max<int64_t>(4 * raw_len, int64_t(64) << 10));
+		hash_wait();  // the staging may still be hashed
+		stage.reserve(size_t(cap));
+		stage_st.reserve(sizeof(lz4ada_block_status));
+		HIP_OK(hipMemcpyAsync(stage_st.p, d_bst.p, sizeof(lz4ada_block_status), hipMemcpyDeviceToHost,
+		                      stream));
+		HIP_OK(hipMemcpyAsync(stage.p, d_buf.p + start, size_t(spec), hipMemcpyDeviceToHost, stream));
+		HIP_OK(hipStreamSynchronize(stream));
+		lz4ada_block_status st;
+		memcpy(&st, stage_st.p, sizeof st);
+		if (st.code != DS_OK)
+			return LONE_DECLINED;
+		const int64_t nout = int64_t(st.out_len);
+		if (nout > spec) {
+			HIP_OK(hipMemcpyAsync(stage.p + spec, d_buf.p + start + spec, size_t(nout - spec),
+			                      hipMemcpyDeviceToHost, stream));
+			HIP_OK(hipStreamSynchronize(stream));
+		}
+		if (m.has_content_size)
+			m.size_remaining -= uint64_t(nout);
+		output_pos = start + nout;
+		if (output_pos >= HISTORY_SIZE)  // :785-787
+			output_pos_history = output_pos;
+		first = start;
+		last = start + nout - 1;
+		if (nout > 0)
+			to_caller(buf + first, nout);
+		return LONE_DONE;
+	}
+
 	int64_t launch_fast_block(int64_t raw_len, int64_t blen, int64_t buflen)
 	{
 		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
@@ -847,23 +1025,8 @@ struct lz4ada_decompressor {
 		if (buflen - start <= 0 || raw_len > INT32_MAX)
 			return -1;
 		const int64_t cap = std::max<int64_t>(block_room(buflen - start, raw_len, m.is_compressed), 1);
-		if (linked && m.is_compressed) {
-			// a linked frame's block: the lone-block decoder with the
-			// reference's history as readable words in front of its output
-			// (every block size; a reference past the history, D1 risk or any
-			// other decline leaves it to the exact path)
-			if (raw_len <= 0 || cap > (int64_t(1) << 30))
-				return -1;
-			int64_t n0, n1;
-			history_of(start, n0, n1);
-			const int64_t sb = lone_scratch_bytes(raw_len, cap);
-			d_scr.reserve(size_t(cap));
-			d_lone.reserve(size_t(sb));
-			HIP_OK(launch_decode_lone(d_blk.p, raw_len, d_scr.p, cap, d_bst.p, d_lone.p, sb, stream,
-			                          d_buf.p + output_pos_history - n0, int32_t(n0), d_buf.p,
-			                          int32_t(n1), d1_window() ? 1 : 0));
-			return start;
-		}
+		if (linked && m.is_compressed)
+			return -1;  // lone_block declined it: the exact path
 		d_scr.reserve(size_t(cap));
 		lz4ada_block_desc d{};
 		d.in_off = 0;
@@ -871,14 +1034,6 @@ struct lz4ada_decompressor {
 		d.flags = m.is_compressed ? 0u : LZ4ADA_BLOCK_STORED;
 		d.out_off = 0;
 		d.out_cap = uint32_t(cap);
-		const int fv = facade_variant();
-		if (fv < 0 && m.is_compressed && (raw_len >= LONE_MIN || fv == -2) && raw_len > 0 &&
-		    cap <= (int64_t(1) << 30)) {
-			const int64_t sb = lone_scratch_bytes(raw_len, cap);
-			d_lone.reserve(size_t(sb));
-			HIP_OK(launch_decode_lone(d_blk.p, raw_len, d_scr.p, cap, d_bst.p, d_lone.p, sb, stream));
-			return start;
-		}
 		HIP_OK(hipMemcpyAsync(d_desc.p, &d, sizeof d, hipMemcpyHostToDevice, stream));
 		HIP_OK(launch_decode_variant(d_blk.p, uint64_t(std::max<int64_t>(blen, 1)), d_desc.p, 1,
 		                             d_scr.p, d_bst.p, DEC_PC, stream));

@@ -192,6 +192,16 @@ hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, i
                               lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
                               hipStream_t stream, const uint8_t* d_h0 = nullptr, int32_t n0 = 0,
                               const uint8_t* d_h1 = nullptr, int32_t n1 = 0, int d1_guard = 0);
+// The same in two halves: the parse (steps 1-3: nothing written to d_out,
+// the status set to DS_RETRY on a decline) and the emit (step 4: the bytes
+// to d_out when the status is still OK).  A caller may check something on
+// the host between them, e.g. the block checksum before d_out is touched.
+hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap,
+                                    lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
+                                    hipStream_t stream, const uint8_t* d_h0, int32_t n0,
+                                    const uint8_t* d_h1, int32_t n1, int d1_guard);
+hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ada_block_status* d_st,
+                                   void* d_scratch, hipStream_t stream, int32_t H);
 
 // host side (lz4ada_host.cpp): the calling thread's message for
 // lz4ada_thread_last_error() and its lz4ada_last_path() bits

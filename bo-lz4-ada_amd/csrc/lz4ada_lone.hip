@@ -23,9 +23,10 @@
 //     the windows' output bytes places each window in the output.
 //  3. k_lone_words -- one workgroup per window: marks the true chain from the
 //     window's entry (pointer doubling), places each sequence by a prefix
-//     sum and writes one word per output byte: a literal (bit 31 | byte) or
-//     the output position the byte copies (Output_With_History's byte i =
-//     byte i - offset, which also gives the overlap rule).
+//     sum and writes one word per output byte, in tiles of consecutive words
+//     (coalesced stores): a literal (bit 31 | byte) or the output position
+//     the byte copies (Output_With_History's byte i = byte i - offset, which
+//     also gives the overlap rule).
 //  4. k_lone_resolve -- the copies resolved by pointer jumping over the
 //     words (W[i] = W[W[i]] until every word is a literal), each workgroup
 //     over its own slice of the output, reading the others' slices as they
@@ -38,15 +39,17 @@
 
 namespace lz4ada {
 
-constexpr int32_t LW = 4096;        // compressed bytes per window
-constexpr int32_t LT = 256;         // threads per workgroup
-constexpr int32_t LP = LW / LT;     // positions per thread
-constexpr int32_t LSTG = 2 * LW;    // staged input bytes (window + 4 KiB lookahead)
+// Window size LW (compressed bytes per workgroup in steps 1 and 3): 1, 2 or
+// 4 KiB by the block's compressed size (lone_window, host side).  Small
+// windows give a small block more workgroups; large ones keep the chain
+// step short where speculative chains do not merge (literal-heavy data).
+constexpr int32_t LW_MIN = 1024;
+constexpr int32_t LT = 256;               // threads per workgroup
 constexpr uint32_t NX_BAD = 0xFFFFFFFFu;  // not a sequence (or beyond what a window parses)
 constexpr uint32_t LIT = 0x80000000u;     // word: a literal byte
-constexpr int32_t LONG_SEQ = 64;          // sequences over this many output bytes: whole workgroup
-constexpr int32_t RES_SLICE = 16384;      // output words per workgroup in k_lone_resolve
+constexpr int32_t RES_SLICE = 4096;       // output words per workgroup in k_lone_resolve
 constexpr int32_t MAX_RUN_L = 1 << 28;
+static_assert(RES_SLICE % (4 * LT) == 0, "lone-decoder tiling");
 
 struct LoneCtl {
 	int32_t code;     // DS_OK, or DS_RETRY once any step declines
@@ -224,12 +227,14 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b)
 // Also the entry guess for the next window: the exit most positions of this
 // window reach (chains started at wrong bytes mostly merge into the true
 // one before the window ends), counted in an LDS hash table.
+template <int32_t LW>
 __global__ __launch_bounds__(LT) void k_lone_windows(const uint8_t* __restrict__ blk, int32_t n,
                                                      uint32_t* __restrict__ exit_tab,
                                                      uint32_t* __restrict__ osum_tab,
                                                      uint32_t* __restrict__ nxt_tab,
                                                      uint32_t* __restrict__ guess)
 {
+	constexpr int32_t LP = LW / LT, LSTG = 2 * LW;
 	__shared__ alignas(16) uint8_t s[LSTG + 32];
 	__shared__ uint64_t X[LW];  // nx | os << 32
 	__shared__ uint32_t best[LT / 64][2];
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(LT) void k_lone_windows(const uint8_t* __restrict__
 		const uint32_t e = ex[k];
 		if (e == NX_BAD)
 			continue;
-		uint32_t h = (e * 2654435761u) >> 20;  // 12 bits
+		uint32_t h = (e * 2654435761u) >> (32 - __builtin_ctz(uint32_t(LW)));  // log2(LW) bits
 		for (int probe = 0; probe < LW; ++probe, h = (h + 1) & (LW - 1)) {
 			const uint32_t old = atomicCAS(&key[h], NX_BAD, e);
 			if (old == NX_BAD || old == e) {
@@ -337,8 +342,8 @@ __global__ __launch_bounds__(LT) void k_lone_windows(const uint8_t* __restrict__
 
 // ---------------------------------------------------------------- step 2
 constexpr int32_t CT = 1024;  // k_lone_chain threads
-constexpr int32_t CK = 4;     // windows per thread (nwin <= CT * CK: 16 MiB blocks)
 
+template <int32_t LW>
 __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ exit_tab,
                                                    const uint32_t* __restrict__ osum_tab,
                                                    const uint32_t* __restrict__ guess,
@@ -348,6 +353,7 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
                                                    LoneCtl* __restrict__ ctl,
                                                    lz4ada_block_status* __restrict__ st)
 {
+	constexpr int32_t CK = (int32_t(16) << 20) / LW / CT;  // windows per thread (16 MiB blocks)
 	extern __shared__ uint32_t E[];  // entries 0..nwin
 	__shared__ uint32_t wsum[CT / 64];
 	__shared__ unsigned long long total64;
@@ -447,34 +453,27 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------- step 3
-// Words of output bytes [o, o + q.os) of sequence q: literals (bit 31 | the
-// byte, four per input dword) then the match (the position each byte
-// copies).  Threads j = j0, j0 + js, ... of the caller share the work.
-__device__ __forceinline__ void lone_emit(const LoneSrc& S, const LoneSeq& q, uint32_t o,
-                                          uint32_t* __restrict__ W, int32_t j0, int32_t js,
-                                          int32_t n, uint32_t hb)
-{
-	for (int32_t b = 4 * j0; b < q.L; b += 4 * js) {
-		const int32_t x = q.lit + b;
-		uint32_t d;
-		if (x + 4 <= n) {
-			d = S.at4(x);
-		} else {
-			d = 0;
-			for (int32_t k = 0; k < 4 && x + k < n; ++k)
-				d |= S.at(x + k) << (8 * k);
-		}
-		const int32_t m = min(4, q.L - b);
-#pragma unroll
-		for (int32_t k = 0; k < 4; ++k)
-			if (k < m)
-				W[o + uint32_t(b + k)] = LIT | ((d >> (8 * k)) & 0xFFu);
-	}
-	const uint32_t m0 = o + uint32_t(q.L);
-	for (int32_t b = j0; b < q.ml; b += js)
-		W[m0 + uint32_t(b)] = hb + m0 + uint32_t(b) - uint32_t(q.off);
-}
+// One workgroup per window.  The true chain is marked from the window's
+// entry (pointer doubling), its sequences are parsed once into an LDS table
+// in chain order (output start, literal position, literal length, offset),
+// and the window's output words are written in tiles of OT consecutive
+// words: every sequence starting in the tile marks its first word, a prefix
+// maximum gives every word its sequence, and lane i of a wave writes word
+// i -- each store instruction covers 256 contiguous bytes.  A word is a
+// literal (bit 31 | the byte) or the output position the byte copies
+// (Output_With_History's byte i = byte i - offset, which also gives the
+// overlap rule); H history words precede output byte 0.
+constexpr int32_t OT = 4096;            // output words per emission tile
+constexpr int32_t OTP = OT / LT;        // per thread in the tile's prefix maximum
 
+struct SeqRec {
+	uint32_t o;    // first output byte, from the window's first
+	int32_t lit;   // block position of the first literal
+	int32_t L;     // literal bytes
+	uint32_t off;  // match offset (0: none)
+};
+
+template <int32_t LW>
 __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ blk, int32_t n,
                                                    const uint32_t* __restrict__ nxt_tab,
                                                    const uint32_t* __restrict__ entry,
@@ -485,14 +484,15 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
                                                    int32_t d1_guard)
 {
 	// words [0, H): the history (literals); output byte x is word H + x
+	constexpr int32_t LP = LW / LT, LSTG = 2 * LW;
+	constexpr int32_t MAXSEQ = LW / 3 + 2;  // chain sequences starting in a window (>= 3 bytes but the last)
 	uint32_t* __restrict__ W = Wbase + H;
 	__shared__ alignas(16) uint8_t s[LSTG + 32];
 	__shared__ uint16_t J[LW];
 	__shared__ uint8_t mark[LW];
-	__shared__ uint32_t tsum[LT / 64];
-	__shared__ int32_t nlong;
-	__shared__ int32_t lpos[LW / 4];
-	__shared__ uint32_t lout[LW / 4];
+	__shared__ alignas(16) SeqRec R[MAXSEQ + 1];
+	__shared__ uint16_t T16[OT];
+	__shared__ uint32_t wred[3][LT / 64];
 	if (ctl->code != DS_OK)
 		return;
 	const int32_t w = int32_t(blockIdx.x);
@@ -503,6 +503,7 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 	const int32_t shi = min(ws + LSTG, n);
 	cg8* in = gptr(blk);
 	const int32_t tid = int32_t(threadIdx.x), t0 = tid * LP;
+	const uint32_t lane = lane_id(), wv = uint32_t(tid) >> 6;
 	constexpr uint16_t EXIT = 0xFFFFu;
 	for (int32_t i = tid; i < LW; i += LT) {
 		const int32_t p = ws + i;
@@ -515,14 +516,13 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 		J[i] = j;
 		mark[i] = uint8_t(p == int32_t(e));
 	}
-	if (tid == 0)
-		nlong = 0;
 	lone_stage(s, in, ws, shi);  // ends with a barrier
 	const LoneSrc S{ s, ws, shi, in };
 	// mark the chain from e: after round r every position within 2^(r+1)
 	// steps of e is marked
 	for (int r = 0; r < 12; ++r) {
 		int any = 0;
+#pragma unroll
 		for (int32_t k = 0; k < LP; ++k) {
 			const uint16_t j = J[t0 + k];
 			if (j != EXIT) {
@@ -534,57 +534,66 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 		if (!__syncthreads_or(any))
 			break;
 		uint16_t nj[LP];
+#pragma unroll
 		for (int32_t k = 0; k < LP; ++k) {
 			const uint16_t j = J[t0 + k];
 			nj[k] = j == EXIT ? EXIT : J[j];
 		}
 		__syncthreads();
+#pragma unroll
 		for (int32_t k = 0; k < LP; ++k)
 			J[t0 + k] = nj[k];
 		__syncthreads();
 	}
-	// this thread's marked sequences (the true chain: parsed without bound)
-	LoneSeq qs[LP];
-	uint32_t mine = 0;
+	// this thread's chain sequences, in order: table index by a prefix sum
 	uint32_t mk = 0;
-	for (int32_t k = 0; k < LP; ++k) {
-		if (mark[t0 + k]) {
-			qs[k] = lone_parse(S, ws + t0 + k, n, GMAX_TRUE);
-			mine += qs[k].os;
-			mk |= 1u << k;
-		}
-	}
-	const uint32_t lane = lane_id(), wv = uint32_t(tid) >> 6;
-	const uint32_t inc = uint32_t(wave_incl_scan(int32_t(mine)));
+#pragma unroll
+	for (int32_t k = 0; k < LP; ++k)
+		mk |= uint32_t(mark[t0 + k] != 0) << k;
+	const int32_t cnt = __builtin_popcount(mk);
+	const int32_t ci = wave_incl_scan(cnt);
 	if (lane == 63)
-		tsum[wv] = inc;
-	__syncthreads();
-	uint32_t o = obase[w] + inc - mine;
-	for (uint32_t j = 0; j < wv; ++j)
-		o += tsum[j];
+		wred[0][wv] = uint32_t(ci);
+	// parsed without bound (the true chain); output bytes relative to the
+	// thread's first sequence until the second prefix sum
 	bool bad = false;
-	for (int32_t k = 0; k < LP; ++k) {
-		if (!(mk >> k & 1u))
-			continue;
-		const LoneSeq& q = qs[k];
-		if (q.nx == NX_BAD)
+	uint32_t mine = 0;
+	__syncthreads();
+	int32_t si = ci - cnt, ns = 0;
+	for (uint32_t j = 0; j < LT / 64; ++j) {
+		si += j < wv ? int32_t(wred[0][j]) : 0;
+		ns += int32_t(wred[0][j]);
+	}
+	int32_t sj = si;
+	for (uint32_t m = mk; m; m &= m - 1u, ++sj) {
+		const int32_t k = __builtin_ctz(m);
+		const LoneSeq q = lone_parse(S, ws + t0 + k, n, GMAX_TRUE);
+		if (q.nx == NX_BAD || sj >= MAXSEQ) {
 			bad = true;  // never expected: k_lone_chain accepted this chain
-		else if (q.ml && int64_t(o) + q.L + H < int64_t(q.off))
-			bad = true;  // a reference before the history it was given (exact path)
-		else if (d1_guard && q.ml && int64_t(o) + q.L < int64_t(q.off) && q.off >= D1_OFF)
-			bad = true;  // quirk D1: the reference's wild copy may have clobbered it
-		else if (int32_t(q.os) > LONG_SEQ) {
-			const int32_t i = atomicAdd(&nlong, 1);
-			if (i < LW / 4) {
-				lpos[i] = ws + t0 + k;
-				lout[i] = o;
-			} else {
-				bad = true;  // never expected (a window holds < LW/4 long sequences)
-			}
-		} else {
-			lone_emit(S, q, o, W, 0, 1, n, uint32_t(H));
+			continue;
 		}
-		o += q.os;
+		R[sj] = SeqRec{ mine, q.lit, q.L, uint32_t(q.off) };
+		mine += q.os;
+	}
+	const uint32_t oi = uint32_t(wave_incl_scan(int32_t(mine)));
+	if (lane == 63)
+		wred[1][wv] = oi;
+	__syncthreads();
+	uint32_t ob = oi - mine, tw = 0;
+	for (uint32_t j = 0; j < LT / 64; ++j) {
+		ob += j < wv ? wred[1][j] : 0u;
+		tw += wred[1][j];
+	}
+	const uint32_t wo = obase[w];
+	for (int32_t j = si; j < min(sj, MAXSEQ); ++j) {
+		const uint32_t o = R[j].o + ob;
+		R[j].o = o;
+		const int32_t L = R[j].L;
+		const int64_t off = int64_t(R[j].off), oa = int64_t(wo) + o;
+		if (off && oa + L + H < off)
+			bad = true;  // a reference before the history it was given (exact path)
+		else if (d1_guard && off && oa + L < off && off >= D1_OFF)
+			bad = true;  // quirk D1: the reference's wild copy may have clobbered it
 	}
 	if (__syncthreads_or(bad)) {
 		if (tid == 0) {
@@ -594,11 +603,54 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 		}
 		return;
 	}
-	// long sequences: the whole workgroup, one after the other
-	const int32_t nl = nlong;
-	for (int32_t i = 0; i < nl; ++i) {
-		const LoneSeq q = lone_parse(S, lpos[i], n, GMAX_TRUE);
-		lone_emit(S, q, lout[i], W, tid, LT, n, uint32_t(H));
+	// tiles of the window's output words [wo, wo + tw)
+	uint32_t cur = 0;  // 1 + the sequence covering the tile's first word
+	for (uint32_t tb = 0; tb < tw; tb += OT) {
+#pragma unroll
+		for (int32_t k = 0; k < OTP; ++k)
+			T16[tid + LT * k] = 0;
+		__syncthreads();
+		for (int32_t j = tid; j < ns; j += LT) {
+			const uint32_t o = R[j].o;
+			if (o >= tb && o - tb < uint32_t(OT) && o < tw)
+				T16[o - tb] = uint16_t(j + 1);
+		}
+		__syncthreads();
+		uint32_t v[OTP], run = 0;
+#pragma unroll
+		for (int32_t k = 0; k < OTP; ++k) {
+			run = max(run, uint32_t(T16[tid * OTP + k]));
+			v[k] = run;
+		}
+		const uint32_t inc = uint32_t(wave_incl_max(int32_t(run)));
+		if (lane == 63)
+			wred[2][wv] = inc;
+		uint32_t pre = uint32_t(__shfl_up(int32_t(inc), 1));
+		pre = lane ? pre : 0u;
+		__syncthreads();
+		uint32_t tmax = cur;
+		for (uint32_t j = 0; j < LT / 64; ++j) {
+			pre = j < wv ? max(pre, wred[2][j]) : pre;
+			tmax = max(tmax, wred[2][j]);
+		}
+		pre = max(pre, cur);
+#pragma unroll
+		for (int32_t k = 0; k < OTP; ++k)
+			T16[tid * OTP + k] = uint16_t(max(v[k], pre) - 1u);
+		cur = tmax;
+		__syncthreads();
+		const uint32_t lim = min(uint32_t(OT), tw - tb);
+#pragma unroll 4
+		for (int32_t k = 0; k < OTP; ++k) {
+			const uint32_t i = uint32_t(tid + LT * k);
+			if (i < lim) {
+				const SeqRec r = R[T16[i]];
+				const uint32_t x = tb + i - r.o;
+				const uint32_t oa = wo + tb + i;
+				W[oa] = int32_t(x) < r.L ? (LIT | S.at(r.lit + int32_t(x))) : uint32_t(H) + oa - r.off;
+			}
+		}
+		__syncthreads();
 	}
 }
 
@@ -616,7 +668,7 @@ __device__ __forceinline__ void w_store(uint32_t* p, uint32_t v)
 	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr int32_t RPT = RES_SLICE / LT;  // words per thread (64)
+constexpr int32_t RPT = RES_SLICE / LT;  // words per thread
 
 __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
                                                      const LoneCtl* __restrict__ ctl,
@@ -702,39 +754,66 @@ __global__ __launch_bounds__(LT) void k_lone_hist(uint32_t* __restrict__ W, cons
 // ---------------------------------------------------------------- host side
 int64_t lone_scratch_bytes(int64_t n, int64_t cap)
 {
-	const int64_t nwin = (n + LW - 1) / LW;
+	const int64_t nwin = (n + LW_MIN - 1) / LW_MIN;
 	return 12 * std::max<int64_t>(n, 1) + 12 * (nwin + 2) + 64 + 4 * std::max<int64_t>(cap, 1) +
 	       4 * 65536 + 512;
 }
 
-hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
-                              lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
-                              hipStream_t stream, const uint8_t* d_h0, int32_t n0, const uint8_t* d_h1,
-                              int32_t n1, int d1_guard)
+// Window size by compressed size (tools/lone_time.py, round 4: 256 KiB mixed
+// blocks 0.129 / 0.081 / 0.059 ms at 4 / 2 / 1 KiB windows; 4 MiB mixed
+// 0.222 / 0.177 / 0.376, dense 0.362 / 0.317 / 0.289, literal 0.453 /
+// 0.580 / 0.956).  LZ4ADA_LONE_LW forces one.
+static int32_t lone_window(int64_t n)
 {
+	static const int32_t forced = [] {
+		const char* e = getenv("LZ4ADA_LONE_LW");
+		const int v = e ? atoi(e) : 0;
+		return (v == 1024 || v == 2048 || v == 4096) ? v : 0;
+	}();
+	if (forced)
+		return forced;
+	return n <= (int64_t(1) << 20) ? 1024 : n <= (int64_t(5) << 19) ? 2048 : 4096;
+}
+
+// The scratch: per-position tables, per-window entries, the control block
+// and the words (H history words, then one per output byte).
+struct LoneLayout {
+	uint32_t *exit_tab, *osum_tab, *nxt_tab, *entry, *obase, *guess, *W;
+	LoneCtl* ctl;
+	LoneLayout(uint8_t* sc, int64_t n, int64_t nwin)
+	{
+		exit_tab = reinterpret_cast<uint32_t*>(sc);
+		osum_tab = exit_tab + n;
+		nxt_tab = osum_tab + n;
+		entry = nxt_tab + n;
+		obase = entry + (nwin + 1);
+		guess = obase + (nwin + 1);
+		ctl = reinterpret_cast<LoneCtl*>((reinterpret_cast<uintptr_t>(guess + (nwin + 1)) + 63) &
+		                                 ~uintptr_t(63));
+		W = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(ctl + 1) + 255) & ~uintptr_t(255));
+	}
+};
+
+template <int32_t LW>
+static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ada_block_status* d_st,
+                             uint8_t* sc, hipStream_t stream, const uint8_t* d_h0, int32_t n0,
+                             const uint8_t* d_h1, int32_t n1, int d1_guard)
+{
+	constexpr int32_t CK = (int32_t(16) << 20) / LW / CT;
 	const int64_t nwin = (n + LW - 1) / LW;
-	const int32_t H = n0 + n1;
-	if (n <= 0 || n > (int64_t(1) << 30) || cap <= 0 || cap > (int64_t(1) << 30) ||
-	    nwin > CK * CT || scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 ||
-	    H > 65535)
+	if (nwin > int64_t(CK) * CT)
 		return hipErrorInvalidValue;
-	uint8_t* sc = static_cast<uint8_t*>(d_scratch);
-	uint32_t* exit_tab = reinterpret_cast<uint32_t*>(sc);
-	uint32_t* osum_tab = exit_tab + n;
-	uint32_t* nxt_tab = osum_tab + n;
-	uint32_t* entry = nxt_tab + n;
-	uint32_t* obase = entry + (nwin + 1);
-	uint32_t* guess = obase + (nwin + 1);
-	LoneCtl* ctl = reinterpret_cast<LoneCtl*>(
-	        (reinterpret_cast<uintptr_t>(guess + (nwin + 1)) + 63) & ~uintptr_t(63));
-	uint32_t* W = reinterpret_cast<uint32_t*>(
-	        (reinterpret_cast<uintptr_t>(ctl + 1) + 255) & ~uintptr_t(255));
-	hipLaunchKernelGGL(k_lone_windows, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
+	const int32_t H = n0 + n1;
+	const LoneLayout Lo(sc, n, nwin);
+	uint32_t *exit_tab = Lo.exit_tab, *osum_tab = Lo.osum_tab, *nxt_tab = Lo.nxt_tab, *entry = Lo.entry,
+	         *obase = Lo.obase, *guess = Lo.guess, *W = Lo.W;
+	LoneCtl* ctl = Lo.ctl;
+	hipLaunchKernelGGL(k_lone_windows<LW>, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
 	                   exit_tab, osum_tab, nxt_tab, guess);
 	hipError_t err = hipGetLastError();
 	if (err != hipSuccess)
 		return err;
-	hipLaunchKernelGGL(k_lone_chain, dim3(1), dim3(CT), size_t(nwin + 2) * 4, stream, exit_tab,
+	hipLaunchKernelGGL(k_lone_chain<LW>, dim3(1), dim3(CT), size_t(nwin + 2) * 4, stream, exit_tab,
 	                   osum_tab, guess, int32_t(n), int32_t(nwin), uint32_t(cap), entry, obase, ctl,
 	                   d_st);
 	err = hipGetLastError();
@@ -747,15 +826,48 @@ hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, i
 		if (err != hipSuccess)
 			return err;
 	}
-	hipLaunchKernelGGL(k_lone_words, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
+	hipLaunchKernelGGL(k_lone_words<LW>, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
 	                   nxt_tab, entry, obase, ctl, d_st, W, H, d1_guard);
-	err = hipGetLastError();
-	if (err != hipSuccess)
-		return err;
+	return hipGetLastError();
+}
+
+hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap,
+                                    lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
+                                    hipStream_t stream, const uint8_t* d_h0, int32_t n0,
+                                    const uint8_t* d_h1, int32_t n1, int d1_guard)
+{
+	if (n <= 0 || n > (int64_t(1) << 30) || cap <= 0 || cap > (int64_t(1) << 30) ||
+	    scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 || n0 + n1 > 65535)
+		return hipErrorInvalidValue;
+	uint8_t* sc = static_cast<uint8_t*>(d_scratch);
+	switch (lone_window(n)) {
+	case 1024: return lone_steps<1024>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
+	case 2048: return lone_steps<2048>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
+	default: return lone_steps<4096>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
+	}
+}
+
+hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ada_block_status* d_st,
+                                   void* d_scratch, hipStream_t stream, int32_t H)
+{
+	const int64_t nwin = (n + lone_window(n) - 1) / lone_window(n);
+	const LoneLayout Lo(static_cast<uint8_t*>(d_scratch), n, nwin);
 	const uint32_t nres = uint32_t((cap + RES_SLICE - 1) / RES_SLICE);
-	hipLaunchKernelGGL(k_lone_resolve, dim3(nres), dim3(LT), 0, stream, W, ctl, d_st, d_out,
+	hipLaunchKernelGGL(k_lone_resolve, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st, d_out,
 	                   uint32_t(H));
 	return hipGetLastError();
+}
+
+hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
+                              lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
+                              hipStream_t stream, const uint8_t* d_h0, int32_t n0, const uint8_t* d_h1,
+                              int32_t n1, int d1_guard)
+{
+	const hipError_t err = launch_decode_lone_parse(d_blk, n, cap, d_st, d_scratch, scratch_bytes, stream,
+	                                                d_h0, n0, d_h1, n1, d1_guard);
+	if (err != hipSuccess)
+		return err;
+	return launch_decode_lone_emit(n, d_out, cap, d_st, d_scratch, stream, n0 + n1);
 }
 
 }  // namespace lz4ada

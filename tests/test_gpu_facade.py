@@ -298,3 +298,39 @@ def test_facade_linked_checksum_error_midway(feed):
     bad[descs[3].in_off + 99] ^= 0x11
     tr = same_trace(bytes(bad), feed)
     assert tr[-1][0] == "error" and "CHECKSUM_ERROR" in tr[-1][1]
+
+
+@pytest.mark.parametrize("feed", [0, 4096])
+def test_facade_linked_content_size_short(feed):
+    """A linked frame declaring fewer content bytes than its blocks hold: the
+    lone-block decoder's output room is capped at what the declaration
+    leaves, so the block that overruns it declines before touching the
+    mirror and the exact path raises mid-block, as the reference does."""
+    blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS["mixed"], 5, 256 * KiB, 4)
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], 256 * KiB,
+                                      indep=False, with_content_size=True)
+    hdr_len = len(lz4frame.header(256 * KiB, False, False, False, len(raw)))
+    hdr = lz4frame.header(256 * KiB, False, False, False, len(raw) - 100_000)
+    tr = same_trace(bytes(hdr) + frame[hdr_len:], feed)
+    assert tr[-1][0] == "error"
+
+
+def test_facade_caller_reuses_buffer_between_calls():
+    """The content checksum of a large block runs on a helper thread over the
+    facade's own staging copy, so a caller that overwrites its Buffer as soon
+    as a call returns (it is the caller's memory) cannot break the frame's
+    content checksum."""
+    frame, raw = synth((1, 0, 3), 4, 1 << 20, seed=41, indep=True, block_cksum=True,
+                       content_cksum=True)
+    ctx, pos, mbs = lz4ada.Decompressor.init_with_header(frame)
+    buf = bytearray(mbs)
+    out = bytearray()
+    while pos < len(frame):
+        c, f, l = ctx.update(frame, buf, pos, min(len(frame), pos + 4096))
+        if l >= f:
+            out += buf[f:l + 1]
+            buf[f:l + 1] = bytes(l + 1 - f)
+        pos += c
+        if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
+            break
+    assert bytes(out) == raw
