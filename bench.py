@@ -101,21 +101,55 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def kernel_src_hash() -> str:
-    """sha256 (16 hex digits) of the device-code sources and build flags
-    (bo-lz4-ada_amd/csrc/*.hip, *.h, Makefile): profiles/pmc_decode.json
+def kernel_code_hash(kernel: str = "k_decode_idx", lib: str = None) -> str:
+    """sha256 (16 hex digits) of one kernel's gfx950 machine code and kernel
+    descriptor, read from the built library (the clang offload bundles in
+    liblz4ada_hip.so, the code object's symbol table): profiles/pmc_decode.json
     records the hash it was measured with, and bench.py reports its traffic
-    only when the hash still matches (a kernel change voids the figure)."""
-    import glob
+    only while the hash still matches -- a change to that kernel's code or
+    resources voids the figure, a change elsewhere does not.  None when the
+    library or the kernel is not found."""
     import hashlib
-    h = hashlib.sha256()
-    csrc = os.path.join(ROOT, "bo-lz4-ada_amd", "csrc")
-    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
-                    [os.path.join(csrc, "Makefile")]):
-        h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    import struct
+    lib = lib or os.environ.get("LZ4ADA_LIB") or os.path.join(ROOT, "bo-lz4-ada_amd", "liblz4ada_hip.so")
+    try:
+        with open(lib, "rb") as fh:
+            d = fh.read()
+    except OSError:
+        return None
+    want = f"{len(kernel)}{kernel}E"  # the mangled name's identifier (not its longer relatives)
+    i = 0
+    while True:
+        i = d.find(b"__CLANG_OFFLOAD_BUNDLE__", i)
+        if i < 0:
+            return None
+        n, p = struct.unpack_from("<Q", d, i + 24)[0], i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", d, p)
+            trip = d[p + 24:p + 24 + tl].decode(errors="replace")
+            p += 24 + tl
+            if "gfx950" not in trip or not size:
+                continue
+            elf = d[i + off:i + off + size]
+            shoff, = struct.unpack_from("<Q", elf, 0x28)
+            shentsize, shnum = struct.unpack_from("<HH", elf, 0x3a)
+            secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + k * shentsize) for k in range(shnum)]
+            parts = {}
+            for sym in (s for s in secs if s[1] == 2):  # SHT_SYMTAB
+                strtab = secs[sym[6]]
+                for k in range(sym[5] // 24):
+                    nm, info, _, shndx, val, sz = struct.unpack_from("<IBBHQQ", elf, sym[4] + 24 * k)
+                    name = elf[strtab[4] + nm:elf.index(b"\0", strtab[4] + nm)].decode(errors="replace")
+                    if want in name and 0 < shndx < len(secs) and sz:
+                        sec = secs[shndx]
+                        parts[name] = elf[sec[4] + val - sec[3]:sec[4] + val - sec[3] + sz]
+            if parts:
+                h = hashlib.sha256()
+                for name in sorted(parts):
+                    h.update(name.encode())
+                    h.update(parts[name])
+                return h.hexdigest()[:16]
+        i += 24
 
 
 # ------------------------------------------------------------- synthetic data
@@ -645,10 +679,11 @@ def main():
     if os.path.exists(args.pmc):
         with open(args.pmc) as fh:
             pmc = json.load(fh)
-        # only a figure measured on this workload with these kernel sources
+        # only a figure measured on this workload with this kernel's code
+        code = kernel_code_hash(dec_kernel)
         if (pmc.get("config") == {"kind": args.kind, "blocks": nb, "block_max": bmax}
-                and pmc.get("kernel") == dec_kernel
-                and pmc.get("kernel_src_sha16") == kernel_src_hash()):
+                and pmc.get("kernel") == dec_kernel and code is not None
+                and pmc.get("kernel_code_sha16") == code):
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_src = pmc.get("source")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -659,7 +694,7 @@ def main():
                               "wave) with k_xxh32_rows (block checksums) overlapped on the side "
                               "stream",
             "alg_bytes_per_launch": alg_bytes,
-            "traffic_source": traffic_src, "kernel_src_sha16": kernel_src_hash(),
+            "traffic_source": traffic_src, "kernel_code_sha16": kernel_code_hash(dec_kernel),
             "alone_ms": alone}
 
     if world > 1:

@@ -2284,24 +2284,33 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			}
 			phase("jumps2");
 		} else {
-			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p,
+			// the constant bytes go to F with the words, each round writes the
+			// bytes it resolves: the last round leaves the output
+			F = sink.dst(n);
+			if (!F)
+				return BULK_EXACT;
+			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
 			                        d_ctr.p, stream));
 			d2h(ctr, d_ctr.p, sizeof ctr, stream);
 			phase("init");
+			// span activity flags, double-buffered across rounds
+			const int64_t ns = link_spans(n);
+			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
+			if (!act)
+				return BULK_EXACT;
 			for (int round = 0; ctr[0] > 0; ++round) {
 				if (round > 64)
 					return BULK_EXACT;  // never expected: every pointer goes strictly back
 				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
-				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, d_ctr.p, stream));
+				uint8_t* a_out = act + (round & 1) * ns;
+				const uint8_t* a_in = round ? act + ((round - 1) & 1) * ns : nullptr;
+				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out, d_ctr.p,
+				                        stream));
 				d2h(ctr, d_ctr.p, sizeof ctr, stream);
 				if (ctr[1])
 					return BULK_EXACT;  // a reference before the frame start: the exact error
 			}
-			F = sink.dst(n);
-			if (!F)
-				return BULK_EXACT;
 			phase("jumps");
-			HIP_OK(launch_link_emit(d_P.p, n, F, stream));
 		}
 		HIP_OK(launch_link_tail(F, n, d_tail[cur].p, d_tail[cur ^ 1].p, stream));
 		cur ^= 1;

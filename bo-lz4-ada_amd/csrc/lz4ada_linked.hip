@@ -21,8 +21,9 @@
 //  * k_link_jump resolves the pointers by pointer jumping (each round
 //    replaces a pointer by its target's word, so chains through many
 //    blocks finish in ~log2(length) rounds), reading positions before the
-//    batch from the previous batch's last 64 KiB;
-//  * k_link_emit writes the bytes.
+//    batch from the previous batch's last 64 KiB; k_link_init writes the
+//    constant bytes and each round the bytes it resolves, so the last
+//    round leaves the output (k_link_emit: a separate pass, unused).
 //
 // The result equals decoding the frame with contiguous history.  The
 // reference differs from that only in quirk D1 (wild-copy overshoot into
@@ -81,18 +82,41 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 	}
 }
 
+// 16 bytes at F + a (any alignment).
+__device__ __forceinline__ void f_store16(uint8_t* F, int64_t a, uint32_t o0, uint32_t o1, uint32_t o2,
+                                          uint32_t o3)
+{
+	GLOBAL uint8_t* f = gptr(F) + a;
+	const uintptr_t fa = reinterpret_cast<uintptr_t>(f);
+	if ((fa & 15u) == 0) {
+		*reinterpret_cast<GLOBAL u32x4*>(f) = u32x4{ o0, o1, o2, o3 };
+	} else if ((fa & 3u) == 0) {
+		GLOBAL uint32_t* f4 = reinterpret_cast<GLOBAL uint32_t*>(f);
+		f4[0] = o0;
+		f4[1] = o1;
+		f4[2] = o2;
+		f4[3] = o3;
+	} else {
+		const uint32_t o[4] = { o0, o1, o2, o3 };
+#pragma unroll
+		for (int i = 0; i < 16; ++i)
+			f[i] = uint8_t(o[i >> 2] >> (8 * (i & 3)));
+	}
+}
+
 // One word per output byte of the batch (batch-relative position a =
 // A[b] + q): RES | byte, or the encoded position of the byte it copies,
-// (source position) + 65536 -- always >= 0, and below a.  Four bytes per
-// lane: dword loads of the three copies, one 16-byte store of the words
-// (four dword stores when the block's words are not 16-byte aligned).
+// (source position) + 65536 -- always >= 0, and below a.  Every byte also
+// goes to F (a history-derived one as a placeholder, rewritten by the jump
+// round that resolves it), so no emit pass reads the words again.  16 bytes
+// per lane: dwordx4 loads of the three copies, four 16-byte word stores.
 __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x,
                                                    const uint8_t* __restrict__ y,
                                                    const uint8_t* __restrict__ h,
                                                    const lz4ada_block_desc* __restrict__ desc,
                                                    const lz4ada_block_status* __restrict__ st,
                                                    const int64_t* __restrict__ A, uint32_t nblocks,
-                                                   uint32_t* __restrict__ P,
+                                                   uint32_t* __restrict__ P, uint8_t* __restrict__ F,
                                                    uint32_t* __restrict__ ctr)
 {
 	const uint32_t b = blockIdx.x;
@@ -102,16 +126,19 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 	const int64_t len = st[b].out_len;
 	const int64_t ab = A[b];
 	uint32_t unres = 0;
-	for (int64_t q0 = 4 * (int64_t(blockIdx.y) * TPB + threadIdx.x); q0 < len;
-	     q0 += 4 * int64_t(gridDim.y) * TPB) {
-		const uint32_t wx = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(x) + ob + q0);
-		const uint32_t wy = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(y) + ob + q0);
-		const uint32_t wh = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(h) + ob + q0);
-		uint32_t v[4];
+	for (int64_t q0 = 16 * (int64_t(blockIdx.y) * TPB + threadIdx.x); q0 < len;
+	     q0 += 16 * int64_t(gridDim.y) * TPB) {
+		const u32x4 vx = *reinterpret_cast<const GLOBAL u32x4*>(gptr(x) + ob + q0);
+		const u32x4 vy = *reinterpret_cast<const GLOBAL u32x4*>(gptr(y) + ob + q0);
+		const u32x4 vh = *reinterpret_cast<const GLOBAL u32x4*>(gptr(h) + ob + q0);
+		const uint32_t wx[4] = { vx.x, vx.y, vx.z, vx.w }, wy[4] = { vy.x, vy.y, vy.z, vy.w },
+		               wh[4] = { vh.x, vh.y, vh.z, vh.w };
+		uint32_t v[16];
 #pragma unroll
-		for (int i = 0; i < 4; ++i) {
-			const uint32_t bx = (wx >> (8 * i)) & 255u, by = (wy >> (8 * i)) & 255u;
-			const uint32_t bh = (wh >> (8 * i)) & 255u;
+		for (int i = 0; i < 16; ++i) {
+			const uint32_t bx = (wx[i >> 2] >> (8 * (i & 3))) & 255u;
+			const uint32_t by = (wy[i >> 2] >> (8 * (i & 3))) & 255u;
+			const uint32_t bh = (wh[i >> 2] >> (8 * (i & 3))) & 255u;
 			const bool from_hist = bx != by && q0 + i < len;
 			// history position k = bx | bh << 8 is byte k - 65536 of the
 			// block-relative output: source ab + k - 65536, encoded + 65536
@@ -119,13 +146,19 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 			unres += from_hist ? 1u : 0u;
 		}
 		GLOBAL uint32_t* dst = gptr(P) + ab + q0;
-		if (((ab & 3) == 0) && q0 + 4 <= len) {
-			*reinterpret_cast<GLOBAL u32x4*>(dst) = u32x4{ v[0], v[1], v[2], v[3] };
+		if (((ab & 3) == 0) && q0 + 16 <= len) {
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				*reinterpret_cast<GLOBAL u32x4*>(dst + 4 * j) =
+				        u32x4{ v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3] };
+			f_store16(F, ab + q0, vx.x, vx.y, vx.z, vx.w);
 		} else {
 #pragma unroll
-			for (int i = 0; i < 4; ++i)
-				if (q0 + i < len)
+			for (int i = 0; i < 16; ++i)
+				if (q0 + i < len) {
 					dst[i] = v[i];
+					F[ab + q0 + i] = uint8_t(wx[i >> 2] >> (8 * (i & 3)));
+				}
 		}
 	}
 	wave_count(ctr, unres);
@@ -133,45 +166,99 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 
 // One pointer-jumping round over P[0, n).  ctr[0]: words still unresolved
 // after the round; ctr[1]: references before the frame start (positions
-// below -tail_valid).  tail: the 65536 output bytes before the batch.
+// below -tail_valid).  tail: the 65536 output bytes before the batch.  A
+// lane takes four positions: their words, then every unresolved one's
+// target word, loaded together before any is used; where a word changes the
+// lane rewrites its four bytes of F (the last round to touch them leaves the
+// final bytes).
+//
+// Activity flags: a workgroup pass covers SPAN consecutive positions; act_out
+// gets 1 for a span that still holds an unresolved word after the round, and
+// a later round given act_in skips every span flagged 0 (most of the frame
+// after the first round) instead of reading its words again.
+constexpr int64_t SPAN = 4 * TPB;
+
+// Positions a0 .. a0+3 (a0 < n): one jump of every unresolved word, their
+// bytes to F.  Returns the words still unresolved.
+__device__ __forceinline__ uint32_t jump4(GLOBAL uint32_t* Pg, int64_t a0, int64_t n,
+                                          const uint8_t* __restrict__ tail, int64_t tail_valid,
+                                          uint8_t* __restrict__ F, uint32_t& bad)
+{
+	uint32_t w[4];
+	const bool full = a0 + 4 <= n;
+	if (full) {
+		const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(Pg + a0);
+		w[0] = v.x;
+		w[1] = v.y;
+		w[2] = v.z;
+		w[3] = v.w;
+	} else {
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			w[i] = a0 + i < n ? Pg[a0 + i] : RES;
+	}
+	if ((w[0] & w[1] & w[2] & w[3]) & RES)
+		return 0;  // all resolved (their bytes are in F already)
+	uint32_t f[4];
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		const int64_t t = int64_t(w[i] & ~RES) - HISTORY_SIZE;
+		f[i] = w[i];
+		if (w[i] & RES)
+			continue;
+		if (t >= 0)
+			f[i] = Pg[t];  // the source's word: resolved, or a pointer further back
+		else if (t >= -tail_valid)
+			f[i] = RES | tail[HISTORY_SIZE + t];
+		else
+			f[i] = ~0u;  // before the frame start
+	}
+	uint32_t o = 0, unres = 0;
+#pragma unroll
+	for (int i = 0; i < 4; ++i) {
+		if (f[i] == ~0u) {
+			++bad;
+			f[i] = w[i];
+		}
+		if (f[i] != w[i])
+			Pg[a0 + i] = f[i];
+		unres += (f[i] & RES) ? 0u : 1u;
+		o |= (f[i] & 255u) << (8 * i);
+	}
+	GLOBAL uint8_t* fb = gptr(F) + a0;
+	if (full && (reinterpret_cast<uintptr_t>(fb) & 3u) == 0) {
+		*reinterpret_cast<GLOBAL uint32_t*>(fb) = o;
+	} else {
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			if (a0 + i < n)
+				fb[i] = uint8_t(o >> (8 * i));
+	}
+	return unres;
+}
+
 __global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int64_t n,
                                                    const uint8_t* __restrict__ tail,
-                                                   int64_t tail_valid, uint32_t* __restrict__ ctr)
+                                                   int64_t tail_valid, uint8_t* __restrict__ F,
+                                                   const uint8_t* __restrict__ act_in,
+                                                   uint8_t* __restrict__ act_out,
+                                                   uint32_t* __restrict__ ctr)
 {
 	uint32_t unres = 0, bad = 0;
 	GLOBAL uint32_t* Pg = gptr(P);
-	for (int64_t a0 = 4 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
-	     a0 += 4 * int64_t(gridDim.x) * TPB) {
-		uint32_t w[4];
-		if (a0 + 4 <= n) {
-			const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(Pg + a0);
-			w[0] = v.x;
-			w[1] = v.y;
-			w[2] = v.z;
-			w[3] = v.w;
-		} else {
-#pragma unroll
-			for (int i = 0; i < 4; ++i)
-				w[i] = a0 + i < n ? Pg[a0 + i] : RES;
+	for (int64_t s0 = int64_t(blockIdx.x) * SPAN; s0 < n; s0 += int64_t(gridDim.x) * SPAN) {
+		const int64_t span = s0 / SPAN;
+		if (act_in && !act_in[span]) {
+			if (threadIdx.x == 0)
+				act_out[span] = 0;
+			continue;
 		}
-#pragma unroll
-		for (int i = 0; i < 4; ++i) {
-			if (w[i] & RES)
-				continue;
-			const int64_t t = int64_t(w[i]) - HISTORY_SIZE;
-			uint32_t f;
-			if (t >= 0) {
-				f = Pg[t];  // the source's word: resolved, or a pointer further back
-			} else if (t >= -tail_valid) {
-				f = RES | tail[HISTORY_SIZE + t];
-			} else {
-				++bad;
-				continue;
-			}
-			Pg[a0 + i] = f;
-			if (!(f & RES))
-				++unres;
-		}
+		const int64_t a0 = s0 + 4 * int64_t(threadIdx.x);
+		const uint32_t u = a0 < n ? jump4(Pg, a0, n, tail, tail_valid, F, bad) : 0u;
+		unres += u;
+		const int any = __syncthreads_or(u != 0);
+		if (threadIdx.x == 0)
+			act_out[span] = uint8_t(any);
 	}
 	wave_count(&ctr[0], unres);
 	wave_count(&ctr[1], bad);
@@ -361,16 +448,16 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                            uint32_t* d_ctr, hipStream_t stream)
+                            uint8_t* d_F, uint32_t* d_ctr, hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	// ~16 KiB of output per workgroup (each lane loops ~16 times): a
+	// ~16 KiB of output per workgroup (each lane loops ~4 times): a
 	// million 1 KiB workgroups cost more in dispatch than in work
-	const int64_t per = 16 * 4 * link::TPB;
+	const int64_t per = 4 * 16 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
 	hipLaunchKernelGGL(link::k_link_init, dim3(nblocks, gy), dim3(link::TPB), 0, stream, x, y, h, d_desc,
-	                   d_st, d_A, nblocks, d_P, d_ctr);
+	                   d_st, d_A, nblocks, d_P, d_F, d_ctr);
 	return hipGetLastError();
 }
 
@@ -380,13 +467,16 @@ static uint32_t grid_for(int64_t n, int64_t per_thread)
 	return uint32_t(std::min<int64_t>(8192, std::max<int64_t>(1, (n + per - 1) / per)));
 }
 
+int64_t link_spans(int64_t n) { return (n + link::SPAN - 1) / link::SPAN; }
+
 hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
-                            uint32_t* d_ctr, hipStream_t stream)
+                            uint8_t* d_F, const uint8_t* d_act_in, uint8_t* d_act_out, uint32_t* d_ctr,
+                            hipStream_t stream)
 {
 	if (n <= 0)
 		return hipSuccess;
 	hipLaunchKernelGGL(link::k_link_jump, dim3(grid_for(n, 4)), dim3(link::TPB), 0, stream, d_P, n, d_tail,
-	                   tail_valid, d_ctr);
+	                   tail_valid, d_F, d_act_in, d_act_out, d_ctr);
 	return hipGetLastError();
 }
 

@@ -73,3 +73,16 @@ def test_assemble_shard_device_tiling(first, nblocks, unique):
         assert descs[i].flags == lz4ada.BLOCK_HAS_CKSUM
         pos += len(r[0])
     assert eh == [recs[(first + i) % unique][3] for i in range(nblocks)]
+
+
+def test_kernel_code_hash_guards_traffic_figure():
+    """the PMC traffic figure is reused only while the
+    headline kernel's machine code is the one it was measured with -- the
+    hash is read from the built library's gfx950 code object, per kernel."""
+    import bench
+    h = bench.kernel_code_hash("k_decode_idx")
+    assert h is not None and len(h) == 16
+    assert h == bench.kernel_code_hash("k_decode_idx")
+    assert h != bench.kernel_code_hash("k_decode_idx2")  # not a prefix match
+    assert bench.kernel_code_hash("no_such_kernel") is None
+    assert bench.kernel_code_hash("k_decode_idx", lib="/nonexistent.so") is None

@@ -25,7 +25,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from bench import kernel_src_hash  # noqa: E402
+from bench import kernel_code_hash  # noqa: E402
 KERNELS = ("k_decode_idx2", "k_decode_idx", "k_index", "k_decode_sparse", "k_decode_pc", "k_decode_blocks",
            "k_lone_windows", "k_lone_chain", "k_lone_words", "k_lone_resolve", "k_lone_hist",
            "k_link_fill", "k_link_init", "k_link_jump", "k_link_emit", "k_link_tail",
@@ -145,8 +145,8 @@ def main():
               "fetch_bytes_x2": round(dec["fetch_bytes_x2"]),
               "write_bytes": round(dec["write_bytes"]),
               "avg_ns": dec.get("avg_ns"),
-              # bench.py reuses the figure only while the kernel sources match
-              "kernel_src_sha16": kernel_src_hash(),
+              # bench.py reuses the figure only while the kernel's machine code matches
+              "kernel_code_sha16": "+".join(str(kernel_code_hash(k)) for k in dname.split("+")),
               "source": f"profiles/{args.tag}_pmc.json (tools/profile.sh + tools/pmc_summary.py)"}
         with open(os.path.join(prof, "pmc_decode.json"), "w") as fh:
             json.dump(pj, fh, indent=1)
