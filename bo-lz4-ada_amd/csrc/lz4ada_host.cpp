@@ -2289,21 +2289,29 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			F = sink.dst(n);
 			if (!F)
 				return BULK_EXACT;
-			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
-			                        d_ctr.p, stream));
-			d2h(ctr, d_ctr.p, sizeof ctr, stream);
-			phase("init");
-			// span activity flags, double-buffered across rounds
+			// span activity flags, double-buffered across rounds; with the
+			// init-time step forward (default; LZ4ADA_LINK_FWD=0: off) init
+			// writes the first round's flags
+			static const bool fwd = [] {
+				const char* e = getenv("LZ4ADA_LINK_FWD");
+				return !(e && e[0] == '0');
+			}();
 			const int64_t ns = link_spans(n);
 			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
 			if (!act)
 				return BULK_EXACT;
+			if (fwd)
+				HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
+			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
+			                        d_tail[cur].p, tail_valid, fwd ? act + ns : nullptr, d_ctr.p, stream));
+			d2h(ctr, d_ctr.p, sizeof ctr, stream);
+			phase("init");
 			for (int round = 0; ctr[0] > 0; ++round) {
 				if (round > 64)
 					return BULK_EXACT;  // never expected: every pointer goes strictly back
 				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
 				uint8_t* a_out = act + (round & 1) * ns;
-				const uint8_t* a_in = round ? act + ((round - 1) & 1) * ns : nullptr;
+				const uint8_t* a_in = (round || fwd) ? act + ((round + 1) & 1) * ns : nullptr;
 				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out, d_ctr.p,
 				                        stream));
 				d2h(ctr, d_ctr.p, sizeof ctr, stream);

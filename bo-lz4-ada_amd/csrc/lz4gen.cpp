@@ -3,7 +3,8 @@
 // model, together with their decoded bytes, so that benches and GPU tests
 // need no external compressor on the GPU box.  Block rules honoured: the
 // last sequence is literal-only with >= 12 literals when the block allows,
-// offsets lie in [1, min(pos, 65535)].  kind 4 (chain) is for linked frames.
+// offsets lie in [1, min(pos, 65535)].  kind 4 (chain) is for linked frames,
+// kind 5 is mixed with offsets <= 65528 (no quirk-D1 matches).
 #include <stdint.h>
 #include <string.h>
 
@@ -100,6 +101,10 @@ static int64_t gen_block(int kind, uint64_t seed, uint8_t* raw, int64_t raw_len,
 			L = 0;
 			ml = 4 + r.geo(100.0);
 			break;
+		case 5:  // mixed, offsets below 65529: no match can meet quirk D1
+			L = r.geo(12.0);
+			ml = 4 + r.geo(16.0);
+			break;
 		default:  // literal-heavy
 			L = 64 + r.geo(400.0);
 			ml = 4 + r.geo(3.0);
@@ -122,12 +127,13 @@ static int64_t gen_block(int kind, uint64_t seed, uint8_t* raw, int64_t raw_len,
 		}
 		pos += L;
 		if (ml) {
-			const int64_t maxoff = pos + hist < 65535 ? pos + hist : 65535;
+			const int64_t cap = kind == 5 ? 65528 : 65535;
+			const int64_t maxoff = pos + hist < cap ? pos + hist : cap;
 			if (kind == 2)
 				off = 1;
 			else if (kind == 4)
 				off = 1 + r.below(uint32_t(maxoff < 16 ? maxoff : 16));
-			else if (kind == 1 && r.below(4) == 0)
+			else if ((kind == 1 || kind == 5) && r.below(4) == 0)
 				off = 1 + r.below(uint32_t(maxoff < 64 ? maxoff : 64));
 			else
 				off = 1 + r.below(uint32_t(maxoff));

@@ -587,9 +587,9 @@ def output_checksums_device(d_out, d_descs, d_status, nblocks, d_hash, stream=0)
 
 # ---------------------------------------------------------- synthetic data
 
-GEN_DENSE, GEN_MIXED, GEN_RLE, GEN_LITERAL, GEN_CHAIN = 0, 1, 2, 3, 4
+GEN_DENSE, GEN_MIXED, GEN_RLE, GEN_LITERAL, GEN_CHAIN, GEN_MIXED_NOD1 = 0, 1, 2, 3, 4, 5
 GEN_KINDS = {"dense": GEN_DENSE, "mixed": GEN_MIXED, "rle": GEN_RLE, "literal": GEN_LITERAL,
-             "chain": GEN_CHAIN}
+             "chain": GEN_CHAIN, "mixed_nod1": GEN_MIXED_NOD1}
 
 
 def gen_block(kind: int, seed: int, raw_len: int):

@@ -394,7 +394,9 @@ int lz4ada_abi_version(void);
  * Deterministic synthetic LZ4 block generator for benches and tests
  * (SURVEY §8d): emits one valid compressed block whose decoded size is
  * exactly raw_len.  kind: 0 dense (~5 B/sequence), 1 mixed (~32 B/seq,
- * ratio ~2), 2 rle (zeros, offset 1), 3 literal-heavy.  Writes the decoded
+ * ratio ~2), 2 rle (zeros, offset 1), 3 literal-heavy, 4 chain (matches
+ * only, offsets <= 16), 5 mixed with offsets <= 65528 (no match can meet
+ * quirk D1 in a linked frame).  Writes the decoded
  * bytes to raw (raw_len bytes) and the block payload to comp; returns the
  * payload length, or -1 if comp_cap is too small.
  */

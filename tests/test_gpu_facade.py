@@ -334,3 +334,16 @@ def test_facade_caller_reuses_buffer_between_calls():
         if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
             break
     assert bytes(out) == raw
+
+
+@pytest.mark.parametrize("feed", [4096, 0])
+def test_facade_linked_64k_blocks_without_d1_stay_on_gpu(feed):
+    """Linked 64 KiB blocks (the LZ4F default) end every round at exactly
+    65,536, so only a match reaching >= 65,529 back can meet quirk D1; with
+    none (generator kind 5), no block may take the exact path."""
+    frame, raw = linked_frame("mixed_nod1", 64 * KiB, 12, seed=91, last=20_000,
+                              block_cksum=True, content_cksum=True)
+    ours, exact = trace_ours_ctx(frame, feed)
+    assert ours == trace_oracle(frame, feed)
+    assert b"".join(t[3] for t in ours if len(t) == 5) == raw
+    assert exact == 0, exact

@@ -20,6 +20,7 @@ for i in 1 2; do
 timeout -k 10 200 python tools/facade_time.py --indep 0 --block-max 262144 --blocks 32 --feed 4096 --reps 5 2>&1 | grep -v amdgpu
 timeout -k 10 200 python tools/facade_time.py --indep 1 --block-max 65536 --blocks 64 --feed 4096 --reps 5 2>&1 | grep -v amdgpu
 timeout -k 10 200 python tools/facade_time.py --indep 0 --block-max 65536 --blocks 64 --feed 4096 --reps 5 --ccksum 0 2>&1 | grep -v amdgpu
+timeout -k 10 200 python tools/facade_time.py --kind mixed_nod1 --indep 0 --block-max 65536 --blocks 64 --feed 4096 --reps 5 2>&1 | grep -v amdgpu
 timeout -k 10 200 python tools/facade_time.py --indep 1 --block-max 4194304 --blocks 8 --feed 4096 --reps 3 2>&1 | grep -v amdgpu
 done
 LZ4ADA_TRACE_FACADE=1 timeout -k 10 200 python tools/facade_time.py --indep 0 --block-max 262144 --blocks 6 --feed 4096 --reps 1 > $O/trace.log 2>&1
