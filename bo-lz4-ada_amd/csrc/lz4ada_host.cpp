@@ -2290,11 +2290,13 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			if (!F)
 				return BULK_EXACT;
 			// span activity flags, double-buffered across rounds; with the
-			// init-time step forward (default; LZ4ADA_LINK_FWD=0: off) init
-			// writes the first round's flags
+			// init-time step forward (LZ4ADA_LINK_FWD=1) init writes the first
+			// round's flags.  Off by default (tools/r04_linked.sh, 1 GiB of
+			// 256 KiB blocks: mixed 10.32 vs 10.35 ms, chain 13.5 vs 15.4,
+			// dense 31.0 vs 23.7 -- its byte gathers cost what the round saves)
 			static const bool fwd = [] {
 				const char* e = getenv("LZ4ADA_LINK_FWD");
-				return !(e && e[0] == '0');
+				return e && e[0] == '1';
 			}();
 			const int64_t ns = link_spans(n);
 			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
