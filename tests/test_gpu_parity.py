@@ -526,3 +526,43 @@ def test_linked_frame_64k():
     assert st_o == O.OK, msg
     dec, consumed = lz4ada.decode_frame(frame)
     assert dec == ref
+
+
+@pytest.mark.parametrize("nblocks", [40, 1100])  # two-wave (<= 4 x CUs) and one-wave fused decoder
+def test_stored_blocks_hashed_while_copied(nblocks):
+    """Stored blocks with B.Checksum: the index decoders compute the block
+    checksum as they copy the payload (wave_copy_xxh32; k_xxh32_rows skips
+    them) -- every size class of the 16-byte stripe loop and its tail,
+    against the frame's declared checksums and the oracle."""
+    torch = pytest.importorskip("torch")
+    sizes = [1, 15, 16, 17, 255, 1000, 8191, 8192, 8193, 20000, 65536]
+    blocks = []
+    for i in range(nblocks):
+        raw = random.Random(900 + i).randbytes(sizes[i % len(sizes)])
+        blocks.append((raw, raw, True))
+    frame, raw = lz4frame.build_frame(blocks, 64 << 10, block_cksum=True)
+    info, descs = lz4ada.frame_index(frame)
+    nb = info.nblocks
+    dev = torch.device("cuda:0")
+    d_frame = torch.frombuffer(bytearray(frame), dtype=torch.uint8).to(dev)
+    d_desc = torch.frombuffer(bytearray(bytes(descs)[:nb * 32]), dtype=torch.uint8).to(dev)
+    d_out = torch.zeros(nb * info.block_max, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
+    lz4ada.decode_blocks_device(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
+                                d_out.data_ptr(), d_st.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    st = (lz4ada.BlockStatus * nb).from_buffer_copy(d_st.cpu().numpy().tobytes())
+    out = d_out.cpu().numpy().tobytes()
+    for i in range(nb):
+        assert st[i].code == 0 and st[i].out_len == descs[i].in_len
+        assert st[i].cksum == descs[i].cksum, i
+        o = descs[i].out_off
+        assert out[o:o + st[i].out_len] == blocks[i][1]
+    # a corrupted stored block: the reference's checksum error, at that block
+    bad = bytearray(frame)
+    bad[descs[nblocks // 2].in_off + 3] ^= 0x40
+    with pytest.raises(lz4ada.ChecksumError) as ei:
+        lz4ada.decode_frame(bytes(bad))
+    stx, msg = O.error_harness(bytes(bad))
+    assert str(ei.value) == O.exception_information(stx, msg)
