@@ -744,85 +744,6 @@ __device__ __forceinline__ void wave_literal(g8* ob, int32_t dst, const Src& S, 
 	}
 }
 
-// A stored block's copy together with its block checksum (XXH32 seed 0 of
-// the payload, lz4ada.adb:698-707, 979-1017 -- for a stored block the
-// payload is the output).  k_xxh32_rows needs ~55 cycles per 16-byte stripe
-// (its four blocks per wave walk the chain through DPP hand-offs, and the
-// wave's loads in flight bound it); here the wave that copies the block
-// already holds every word: per 8 KiB step each lane multiplies its four
-// words by P2 (the chain's off-chain half, all 64 lanes at once) and writes
-// them transposed into LDS -- row a = accumulator a's words in stripe order
-// -- and lanes 0-3 then run the 512-stripe chain from LDS, four stripes per
-// ds_read_b128: three dependent VALU per stripe (add, v_alignbit, mul; ~17
-// cycles, tools/xxh_latency.hip) while the next step's loads are in flight.
-// T: 2048 words of LDS.  Returns the hash in every lane.
-__device__ __forceinline__ uint32_t wave_copy_xxh32(g8* ob, const Src& S, int32_t len, uint32_t* T)
-{
-	const int32_t lane = int32_t(lane_id());
-	constexpr int U = 8;
-	constexpr int SPS = 64 * U;  // stripes per step
-	const int32_t nstripes = len >> 4;
-	const uint32_t init[4] = { P1 + P2, P2, 0u, 0u - P1 };
-	uint32_t acc = init[lane & 3];
-	u32x4 v[U];
-	auto load = [&](int32_t c) {
-#pragma unroll
-		for (int u = 0; u < U; ++u) {
-			const int32_t k = c + 1024 * u + 16 * lane;
-			v[u] = k < len ? gload16(reinterpret_cast<uintptr_t>(S.in) + uintptr_t(k), S.lim) : u32x4{ 0, 0, 0, 0 };
-		}
-	};
-	if (len > 0)
-		load(0);
-	for (int32_t c = 0; c < len; c += 1024 * U) {
-#pragma unroll
-		for (int u = 0; u < U; ++u) {
-			const int32_t k = c + 1024 * u + 16 * lane;
-			if (k < len)
-				gstore_n(ob + k, v[u], min(16, len - k));
-			const int32_t j = 64 * u + lane;
-			T[j] = v[u].x * P2;
-			T[SPS + j] = v[u].y * P2;
-			T[2 * SPS + j] = v[u].z * P2;
-			T[3 * SPS + j] = v[u].w * P2;
-		}
-		wave_lds_fence();
-		if (c + 1024 * U < len)
-			load(c + 1024 * U);  // in flight while the chain runs
-		const int32_t ns = min(SPS, nstripes - (c >> 4));  // whole stripes of this step
-		if (lane < 4) {
-			const uint32_t* row = T + lane * SPS;
-			int32_t s = 0;
-			for (; s + 4 <= ns; s += 4) {
-				const u32x4 x = *reinterpret_cast<const u32x4*>(row + s);
-				acc = rotl32(acc + x.x, 13) * P1;
-				acc = rotl32(acc + x.y, 13) * P1;
-				acc = rotl32(acc + x.z, 13) * P1;
-				acc = rotl32(acc + x.w, 13) * P1;
-			}
-			for (; s < ns; ++s)
-				acc = rotl32(acc + row[s], 13) * P1;
-		}
-		wave_lds_fence();
-	}
-	const uint32_t v0 = __shfl(acc, 0), v1 = __shfl(acc, 1), v2 = __shfl(acc, 2), v3 = __shfl(acc, 3);
-	uint32_t h = uint32_t(len);
-	h += len >= 16 ? rotl32(v0, 1) + rotl32(v1, 7) + rotl32(v2, 12) + rotl32(v3, 18) : P5;
-	cg8* t = S.in + (nstripes << 4);
-	const int32_t tl = len - (nstripes << 4);
-	int32_t d = 0;
-	for (; d + 4 <= tl; d += 4) {
-		const uint32_t w = uint32_t(t[d]) | (uint32_t(t[d + 1]) << 8) | (uint32_t(t[d + 2]) << 16) |
-		                   (uint32_t(t[d + 3]) << 24);
-		h = rotl32(h + w * P3, 17) * P4;
-	}
-	for (; d < tl; ++d)
-		h = rotl32(h + uint32_t(t[d]) * P5, 11) * P1;
-	h = (h ^ (h >> 15)) * P2;
-	h = (h ^ (h >> 13)) * P3;
-	return h ^ (h >> 16);
-}
-
 // Deferred work item of one lane: a long literal run (src >= 0: input
 // position) or a match (src = -offset) that is long or reads this batch.
 struct Item {
@@ -1402,15 +1323,12 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			Src S0;
 			S0.in = in;
 			S0.lim = lim;
-			// with a block checksum: the copy computes it (k_xxh32_rows skips
-			// stored blocks on this path); else a nontemporal copy
-			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM) {
-				const uint32_t h = wave_copy_xxh32(ob, S0, n, reinterpret_cast<uint32_t*>(oring_of(D)));
-				if (lane == 0)
-					status[b].cksum = h;
-			} else {
+			// nontemporal copy unless the block checksum kernel beside this
+			// one reads the same payload (it then finds it in the caches)
+			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM)
+				wave_literal<0>(ob, 0, S0, 0, n);
+			else
 				wave_literal<LZ4ADA_STORED_NT>(ob, 0, S0, 0, n);
-			}
 		}
 		if (lane == 0) {
 			status[b].code = code;
@@ -2235,22 +2153,16 @@ __device__ __forceinline__ void decode_block2(DecLds2& L, const uint8_t* __restr
 		int32_t code = DS_OK;
 		if (n > cap) {
 			code = DS_OUT_OVERFLOW;
-		} else {
+		} else {  // each wave copies half
 			Src S0;
 			S0.in = in;
 			S0.lim = lim;
-			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM) {
-				// one serial checksum chain: wave 0 copies and hashes the block
-				if (w == 0) {
-					const uint32_t h = wave_copy_xxh32(ob, S0, n, reinterpret_cast<uint32_t*>(L.oring));
-					if (lane == 0)
-						status[b].cksum = h;
-				}
-			} else {  // each wave copies half
-				const int32_t mid = (n >> 1) & ~1023;
-				const int32_t c0 = w == 0 ? 0 : mid, c1 = w == 0 ? mid : n;
+			const int32_t mid = (n >> 1) & ~1023;
+			const int32_t c0 = w == 0 ? 0 : mid, c1 = w == 0 ? mid : n;
+			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM)
+				wave_literal<0>(ob, c0, S0, c0, c1 - c0);
+			else
 				wave_literal<LZ4ADA_STORED_NT>(ob, c0, S0, c0, c1 - c0);
-			}
 		}
 		if (tid == 0) {
 			status[b].code = code;

@@ -129,12 +129,9 @@ hipError_t launch_decode_sparse(const uint8_t* d_frame, uint64_t frame_len,
                                 lz4ada_block_status* d_status, hipStream_t stream);
 
 // Per-block XXH32 of the compressed payloads (block checksums).
-// skip_stored: leave stored blocks to the index decoders, which hash them
-// while they copy them (k_decode_idx / k_decode_idx2).
 hipError_t launch_block_checksums(const uint8_t* d_frame,
                                   const lz4ada_block_desc* d_desc, uint32_t nblocks,
-                                  lz4ada_block_status* d_status, hipStream_t stream,
-                                  int skip_stored = 0);
+                                  lz4ada_block_status* d_status, hipStream_t stream);
 
 // Block checksums and the default decoder together: the checksum kernel
 // (latency-bound, no LDS) runs on a side stream beside pass 1 of the

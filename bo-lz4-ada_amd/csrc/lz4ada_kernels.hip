@@ -1535,9 +1535,8 @@ hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
 		                                   idx_fused_mode(nblocks), stream)
 		           : launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab),
 		                          d_status, stream);
-	// fused: the index decoder hashes the stored blocks as it copies them
 	if (err == hipSuccess)
-		err = launch_block_checksums(d_frame, d_desc, nblocks, d_status, side->s, fuse ? 1 : 0);
+		err = launch_block_checksums(d_frame, d_desc, nblocks, d_status, side->s);
 	if (err == hipSuccess)
 		err = hipEventRecord(side->join, side->s);
 	if (err == hipSuccess && !fuse)

@@ -296,14 +296,12 @@ __device__ __forceinline__ uint32_t xxh32_rows(cg8* p, uint64_t n, cg32* fallbac
 // out == nullptr: block checksums of the compressed data (blocks with
 // B.Checksum; st[b].cksum).  Else: XXH32 of each block's decoded output
 // (st[b].out_len bytes at out + out_off) into hash[b].
-// skip_stored: stored blocks are left out (the index decoders hash them
-// while they copy them, wave_copy_xxh32).
 __global__ __launch_bounds__(64) void k_xxh32_rows(const uint8_t* __restrict__ frame,
                                                    const uint8_t* __restrict__ out,
                                                    const lz4ada_block_desc* __restrict__ desc,
                                                    uint32_t nblocks,
                                                    lz4ada_block_status* __restrict__ st,
-                                                   uint32_t* __restrict__ hash, int skip_stored)
+                                                   uint32_t* __restrict__ hash)
 {
 	const uint32_t lane = lane_id();
 	const uint32_t b = blockIdx.x * XG + (lane >> 4);
@@ -316,8 +314,7 @@ __global__ __launch_bounds__(64) void k_xxh32_rows(const uint8_t* __restrict__ f
 			p = gptr(out) + d.out_off;
 			n = st[b].out_len;
 			want = true;
-		} else if ((d.flags & LZ4ADA_BLOCK_HAS_CKSUM) &&
-		           !(skip_stored && (d.flags & LZ4ADA_BLOCK_STORED))) {
+		} else if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM) {
 			p = gptr(frame) + d.in_off;
 			n = d.in_len;
 			want = true;
@@ -383,13 +380,12 @@ __global__ __launch_bounds__(64) void k_xxh32_update(lz4ada_xxh32_state* __restr
 
 hipError_t launch_block_checksums(const uint8_t* d_frame, const lz4ada_block_desc* d_desc,
                                   uint32_t nblocks, lz4ada_block_status* d_status,
-                                  hipStream_t stream, int skip_stored)
+                                  hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
 	hipLaunchKernelGGL(k_xxh32_rows, dim3((nblocks + XG - 1) / XG), dim3(64), 0, stream, d_frame,
-	                   (const uint8_t*)nullptr, d_desc, nblocks, d_status, (uint32_t*)nullptr,
-	                   skip_stored);
+	                   (const uint8_t*)nullptr, d_desc, nblocks, d_status, (uint32_t*)nullptr);
 	return hipGetLastError();
 }
 
@@ -401,7 +397,7 @@ hipError_t launch_output_checksums(const uint8_t* d_out, const lz4ada_block_desc
 		return hipSuccess;
 	hipLaunchKernelGGL(k_xxh32_rows, dim3((nblocks + XG - 1) / XG), dim3(64), 0, stream,
 	                   (const uint8_t*)nullptr, d_out, d_desc, nblocks,
-	                   const_cast<lz4ada_block_status*>(d_status), d_hash, 0);
+	                   const_cast<lz4ada_block_status*>(d_status), d_hash);
 	return hipGetLastError();
 }
 

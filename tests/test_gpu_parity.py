@@ -530,9 +530,9 @@ def test_linked_frame_64k():
 
 @pytest.mark.parametrize("nblocks", [40, 1100])  # two-wave (<= 4 x CUs) and one-wave fused decoder
 def test_stored_blocks_hashed_while_copied(nblocks):
-    """Stored blocks with B.Checksum: the index decoders compute the block
-    checksum as they copy the payload (wave_copy_xxh32; k_xxh32_rows skips
-    them) -- every size class of the 16-byte stripe loop and its tail,
+    """Stored blocks with B.Checksum through the fused decoders (two-wave
+    and one-wave): copied by the decoder, hashed beside it -- every size
+    class of the 16-byte stripe loop and its tail, every payload alignment,
     against the frame's declared checksums and the oracle."""
     torch = pytest.importorskip("torch")
     sizes = [1, 15, 16, 17, 255, 1000, 8191, 8192, 8193, 20000, 65536]
