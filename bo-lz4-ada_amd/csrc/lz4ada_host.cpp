@@ -14,6 +14,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <future>
+#include <tuple>
 #include <mutex>
 #include <thread>
 #include <cstdarg>
@@ -104,10 +105,109 @@ static void device_check_or_raise()
 		      "no usable HIP device: the LZ4Ada MI355X decoder has no CPU fallback");
 }
 
+// Process-wide pools of the small device and pinned host allocations and
+// of the facade's streams.  A streaming context per frame (tool_unlz4ada
+// re-inits per frame, unlz4ada.adb:84-87) otherwise pays stream creation
+// and a dozen hipMalloc / hipHostMalloc calls per frame -- ~3.5 ms, more
+// than a 4 MiB frame of 64 KiB blocks takes to decode (tools/facade_c).
+// Blocks up to POOL_MAX bytes are kept by power-of-two size class, at most
+// POOL_KEEP bytes per kind and device; a block is pooled only after a
+// device synchronisation (the implicit one of the hipFree it replaces), so
+// no queued work still uses it.  lz4ada_release_device_cache() empties them.
+struct MemPool {
+	static constexpr size_t POOL_MAX = size_t(256) << 20, POOL_KEEP = size_t(1) << 30;
+	std::mutex mu;
+	std::vector<std::tuple<int, size_t, void*>> free;  // (device, class bytes, block)
+	size_t kept = 0;
+	bool pinned;
+	explicit MemPool(bool pin) : pinned(pin) {}
+	static size_t size_class(size_t b)
+	{
+		size_t c = 4096;
+		while (c < b)
+			c <<= 1;
+		return c;
+	}
+	void raw_free(void* p) { (void)(pinned ? hipHostFree(p) : hipFree(p)); }
+	// -> (block, its usable bytes)
+	std::pair<void*, size_t> get(size_t bytes)
+	{
+		int dev = 0;
+		if (!pinned)
+			(void)hipGetDevice(&dev);
+		const size_t c = bytes <= POOL_MAX ? size_class(bytes) : bytes;
+		if (c <= POOL_MAX) {
+			std::lock_guard<std::mutex> l(mu);
+			for (size_t i = 0; i < free.size(); ++i)
+				if (std::get<0>(free[i]) == dev && std::get<1>(free[i]) == c) {
+					void* p = std::get<2>(free[i]);
+					free[i] = free.back();
+					free.pop_back();
+					kept -= c;
+					return { p, c };
+				}
+		}
+		void* p = nullptr;
+		hipError_t e = pinned ? hipHostMalloc(&p, c, hipHostMallocDefault) : hipMalloc(&p, c);
+		if (e != hipSuccess) {  // the pool's idle blocks first, then once more
+			(void)hipGetLastError();
+			release_all();
+			e = pinned ? hipHostMalloc(&p, c, hipHostMallocDefault) : hipMalloc(&p, c);
+		}
+		HIP_OK(e);
+		return { p, c };
+	}
+	void put(void* p, size_t c)
+	{
+		if (!p)
+			return;
+		int dev = 0;
+		if (!pinned)
+			(void)hipGetDevice(&dev);
+		if (c > POOL_MAX || c != size_class(c) || hipDeviceSynchronize() != hipSuccess) {
+			raw_free(p);
+			return;
+		}
+		std::lock_guard<std::mutex> l(mu);
+		if (kept + c > POOL_KEEP) {
+			raw_free(p);
+			return;
+		}
+		free.emplace_back(dev, c, p);
+		kept += c;
+	}
+	void release_all()
+	{
+		std::lock_guard<std::mutex> l(mu);
+		int cur = 0;
+		(void)hipGetDevice(&cur);
+		for (auto& f : free) {
+			if (!pinned)
+				(void)hipSetDevice(std::get<0>(f));
+			raw_free(std::get<2>(f));
+		}
+		if (!pinned)
+			(void)hipSetDevice(cur);
+		free.clear();
+		kept = 0;
+	}
+};
+static MemPool& dev_pool()
+{
+	static MemPool* p = new MemPool(false);  // never destroyed: process lifetime
+	return *p;
+}
+static MemPool& pin_pool()
+{
+	static MemPool* p = new MemPool(true);
+	return *p;
+}
+
 template <class T>
 struct DevBuf {
 	T* p = nullptr;
-	size_t n = 0;  // elements
+	size_t n = 0;      // elements
+	size_t bytes = 0;  // the block's usable bytes
 	DevBuf() = default;
 	DevBuf(const DevBuf&) = delete;
 	DevBuf& operator=(const DevBuf&) = delete;
@@ -115,16 +215,18 @@ struct DevBuf {
 	void release()
 	{
 		if (p)
-			(void)hipFree(p);
+			dev_pool().put(p, bytes);
 		p = nullptr;
-		n = 0;
+		n = bytes = 0;
 	}
 	void reserve(size_t count)
 	{
 		if (count <= n && p)
 			return;
 		release();
-		HIP_OK(hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T) + 64));
+		const auto b = dev_pool().get(std::max<size_t>(count, 1) * sizeof(T) + 64);
+		p = static_cast<T*>(b.first);
+		bytes = b.second;
 		n = count;
 	}
 };
@@ -132,27 +234,37 @@ struct DevBuf {
 // Pinned host memory, grow-only (the facade's output staging).
 struct PinBuf {
 	uint8_t* p = nullptr;
-	size_t n = 0;
+	size_t n = 0, bytes = 0;
 	PinBuf() = default;
 	PinBuf(const PinBuf&) = delete;
 	PinBuf& operator=(const PinBuf&) = delete;
-	~PinBuf()
-	{
-		if (p)
-			(void)hipHostFree(p);
-	}
+	~PinBuf() { pin_pool().put(p, bytes); }
 	void reserve(size_t count)
 	{
 		if (count <= n && p)
 			return;
-		if (p)
-			(void)hipHostFree(p);
+		pin_pool().put(p, bytes);
 		p = nullptr;
-		n = 0;
-		HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1), hipHostMallocDefault));
+		n = bytes = 0;
+		const auto b = pin_pool().get(std::max<size_t>(count, 1));
+		p = static_cast<uint8_t*>(b.first);
+		bytes = b.second;
 		n = count;
 	}
 };
+
+// The facade's streams and event, reused across contexts.
+struct StreamSet {
+	int device = -1;
+	hipStream_t stream = nullptr, side = nullptr;
+	hipEvent_t ev = nullptr;
+};
+static std::mutex g_stream_mu;
+static std::vector<StreamSet>& stream_pool()
+{
+	static std::vector<StreamSet>* v = new std::vector<StreamSet>;  // process lifetime
+	return *v;
+}
 
 // One long-lived helper thread running one job at a time (the facade's
 // content checksum of a large block while the caller feeds the next one);
@@ -579,14 +691,16 @@ struct lz4ada_decompressor {
 	~lz4ada_decompressor()
 	{
 		hash_wait();
-		if (side) {
-			(void)hipStreamSynchronize(side);
+		if (!stream)
+			return;
+		// idle streams go back to the pool for the next context
+		const bool idle = hipStreamSynchronize(side) == hipSuccess && hipStreamSynchronize(stream) == hipSuccess;
+		if (idle) {
+			std::lock_guard<std::mutex> l(g_stream_mu);
+			stream_pool().push_back(StreamSet{ device, stream, side, ev_in });
+		} else {
 			(void)hipStreamDestroy(side);
-		}
-		if (ev_in)
 			(void)hipEventDestroy(ev_in);
-		if (stream) {
-			(void)hipStreamSynchronize(stream);
 			(void)hipStreamDestroy(stream);
 		}
 	}
@@ -597,9 +711,24 @@ struct lz4ada_decompressor {
 			return;
 		device_check_or_raise();
 		HIP_OK(hipGetDevice(&device));
-		HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-		HIP_OK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-		HIP_OK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+		{
+			std::lock_guard<std::mutex> l(g_stream_mu);
+			auto& pool = stream_pool();
+			for (size_t i = 0; i < pool.size(); ++i)
+				if (pool[i].device == device) {
+					stream = pool[i].stream;
+					side = pool[i].side;
+					ev_in = pool[i].ev;
+					pool[i] = pool.back();
+					pool.pop_back();
+					break;
+				}
+		}
+		if (!stream) {
+			HIP_OK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+			HIP_OK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+			HIP_OK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+		}
 		d_tmp_hash.reserve(1);
 		d_serial.reserve(1);
 		d_desc.reserve(1);
@@ -743,6 +872,7 @@ struct lz4ada_decompressor {
 		HIP_OK(hipStreamSynchronize(stream));
 		std::swap(nb.p, d_buf.p);
 		std::swap(nb.n, d_buf.n);
+		std::swap(nb.bytes, d_buf.bytes);
 		d_buf_len = buflen;
 	}
 
@@ -1832,13 +1962,14 @@ static bool try_reserve(DevBuf<T>& b, size_t count)
 	if (count <= b.n && b.p)
 		return true;
 	b.release();
-	if (hipMalloc(reinterpret_cast<void**>(&b.p), std::max<size_t>(count, 1) * sizeof(T) + 64) !=
-	    hipSuccess) {
+	const size_t bytes = std::max<size_t>(count, 1) * sizeof(T) + 64;
+	if (hipMalloc(reinterpret_cast<void**>(&b.p), bytes) != hipSuccess) {
 		(void)hipGetLastError();
 		b.p = nullptr;
 		return false;
 	}
 	b.n = count;
+	b.bytes = bytes;  // not a pool size class: freed, never pooled
 	return true;
 }
 
@@ -2702,7 +2833,12 @@ int lz4ada_decode_linked_device(const void* d_frame, uint64_t frame_len,
 
 int lz4ada_last_path(void) { return g_last_path; }
 
-void lz4ada_release_device_cache(void) { scratch_release(); }
+void lz4ada_release_device_cache(void)
+{
+	scratch_release();
+	dev_pool().release_all();
+	pin_pool().release_all();
+}
 
 int64_t lz4ada_decoded_bound(const uint8_t* input, int64_t len)
 {

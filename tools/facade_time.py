@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--raw-len", type=int, default=0,
                     help="decoded bytes per block (default: --block-max)")
+    ap.add_argument("--dump", default="",
+                    help="also write the frame and its expected output (path, path + '.out') "
+                         "for tools/facade_c (the same loop without Python)")
     args = ap.parse_args()
     n = args.raw_len or args.block_max
     if args.indep:
@@ -67,6 +70,11 @@ def main():
         st, ref, msg = O.unlz4ada(frame, out_cap=len(expect) + (1 << 20))
         assert st == O.OK, f"the reference rejects this frame: {msg} (use --ccksum 0)"
         expect = ref
+    if args.dump:
+        with open(args.dump, "wb") as fh:
+            fh.write(frame)
+        with open(args.dump + ".out", "wb") as fh:
+            fh.write(expect)
     run(frame, expect, args.feed)  # warm
     ts = sorted(run(frame, expect, args.feed) for _ in range(args.reps))
     dt = ts[len(ts) // 2]
