@@ -39,11 +39,11 @@
 
 namespace lz4ada {
 
-// Window size LW (compressed bytes per workgroup in steps 1 and 3): 1, 2 or
-// 4 KiB by the block's compressed size (lone_window, host side).  Small
+// Window size LW (compressed bytes per workgroup in steps 1 and 3): 512 B
+// to 4 KiB by the block's compressed size (lone_window, host side).  Small
 // windows give a small block more workgroups; large ones keep the chain
 // step short where speculative chains do not merge (literal-heavy data).
-constexpr int32_t LW_MIN = 1024;
+constexpr int32_t LW_MIN = 512;
 constexpr int32_t LT = 256;               // threads per workgroup
 constexpr uint32_t NX_BAD = 0xFFFFFFFFu;  // not a sequence (or beyond what a window parses)
 constexpr uint32_t LIT = 0x80000000u;     // word: a literal byte
@@ -759,7 +759,7 @@ int64_t lone_scratch_bytes(int64_t n, int64_t cap)
 	       4 * 65536 + 512;
 }
 
-// Window size by compressed size (tools/lone_time.py, round 4: 256 KiB mixed
+// Window size by compressed size (tools/lone_time.py, tools/r04_lw.sh, round 4: 256 KiB mixed
 // blocks 0.129 / 0.081 / 0.059 ms at 4 / 2 / 1 KiB windows; 4 MiB mixed
 // 0.222 / 0.177 / 0.376, dense 0.362 / 0.317 / 0.289, literal 0.453 /
 // 0.580 / 0.956).  LZ4ADA_LONE_LW forces one.
@@ -768,10 +768,12 @@ static int32_t lone_window(int64_t n)
 	static const int32_t forced = [] {
 		const char* e = getenv("LZ4ADA_LONE_LW");
 		const int v = e ? atoi(e) : 0;
-		return (v == 1024 || v == 2048 || v == 4096) ? v : 0;
+		return (v == 512 || v == 1024 || v == 2048 || v == 4096) ? v : 0;
 	}();
 	if (forced)
 		return forced;
+	if (n <= (int64_t(100) << 10))
+		return 512;  // 64 KiB mixed blocks 0.055 -> 0.049 ms, dense 0.061 -> 0.052 (literal 128 KiB, 130 KB: 0.068 vs 0.077)
 	return n <= (int64_t(1) << 20) ? 1024 : n <= (int64_t(5) << 19) ? 2048 : 4096;
 }
 
@@ -841,6 +843,7 @@ hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap
 		return hipErrorInvalidValue;
 	uint8_t* sc = static_cast<uint8_t*>(d_scratch);
 	switch (lone_window(n)) {
+	case 512: return lone_steps<512>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
 	case 1024: return lone_steps<1024>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
 	case 2048: return lone_steps<2048>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
 	default: return lone_steps<4096>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);

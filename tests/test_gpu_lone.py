@@ -50,8 +50,8 @@ def oracle_block(comp, cap):
 
 
 @pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
-@pytest.mark.parametrize("size", [1, 13, 100, 1023, 1024, 1025, 2047, 2049, 4095, 4096, 4097, 65536,
-                                  300001, 1 << 20, 3 << 20, 4 << 20])
+@pytest.mark.parametrize("size", [1, 13, 100, 511, 512, 513, 1023, 1024, 1025, 2047, 2049, 4095, 4096,
+                                  4097, 65536, 200001, 300001, 1 << 20, 3 << 20, 4 << 20])
 def test_lone_generated_blocks(kind, size):
     comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 0x10E + size, size)
     st, out = run_lone(comp, 4 << 20)
