@@ -180,7 +180,6 @@ int64_t link_spans(int64_t n);
 hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
                             uint8_t* d_F, const uint8_t* d_act_in, uint8_t* d_act_out, uint32_t* d_ctr,
                             hipStream_t stream);
-hipError_t launch_link_emit(const uint32_t* d_P, int64_t n, uint8_t* d_F, hipStream_t stream);
 hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail_old,
                             uint8_t* d_tail_new, hipStream_t stream);
 

@@ -23,7 +23,7 @@
 //    blocks finish in ~log2(length) rounds), reading positions before the
 //    batch from the previous batch's last 64 KiB; k_link_init writes the
 //    constant bytes and each round the bytes it resolves, so the last
-//    round leaves the output (k_link_emit: a separate pass, unused).
+//    round leaves the output (a separate emit pass until round 4).
 //
 // The result equals decoding the frame with contiguous history.  The
 // reference differs from that only in quirk D1 (wild-copy overshoot into
@@ -447,27 +447,6 @@ __global__ __launch_bounds__(TPB) void k_link_jump2(uint32_t* __restrict__ P, co
 	wave_count(&ctr[1], bad);
 }
 
-// Bytes of the resolved words.
-__global__ __launch_bounds__(TPB) void k_link_emit(const uint32_t* __restrict__ P, int64_t n,
-                                                   uint8_t* __restrict__ F)
-{
-	for (int64_t a0 = 16 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
-	     a0 += 16 * int64_t(gridDim.x) * TPB) {
-		if (a0 + 16 <= n) {
-			uint32_t o[4];
-#pragma unroll
-			for (int j = 0; j < 4; ++j) {
-				const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(gptr(P) + a0 + 4 * j);
-				o[j] = (v.x & 255u) | ((v.y & 255u) << 8) | ((v.z & 255u) << 16) | ((v.w & 255u) << 24);
-			}
-			*reinterpret_cast<GLOBAL u32x4*>(gptr(F) + a0) = u32x4{ o[0], o[1], o[2], o[3] };
-		} else {
-			for (int64_t a = a0; a < n; ++a)
-				F[a] = uint8_t(P[a]);
-		}
-	}
-}
-
 // tail_new = the last 65536 bytes of (tail_old ++ F[0, n)).
 __global__ __launch_bounds__(TPB) void k_link_tail(const uint8_t* __restrict__ F, int64_t n,
                                                    const uint8_t* __restrict__ tail_old,
@@ -549,14 +528,6 @@ hipError_t launch_link_jump2(uint32_t* d_P, const uint8_t* d_U, uint8_t* d_F, in
 		return hipSuccess;
 	hipLaunchKernelGGL(link::k_link_jump2, dim3(grid_for(n, 4)), dim3(link::TPB), 0, stream, d_P, d_U, d_F,
 	                   n, d_tail, tail_valid, d_ctr);
-	return hipGetLastError();
-}
-
-hipError_t launch_link_emit(const uint32_t* d_P, int64_t n, uint8_t* d_F, hipStream_t stream)
-{
-	if (n <= 0)
-		return hipSuccess;
-	hipLaunchKernelGGL(link::k_link_emit, dim3(grid_for(n, 16)), dim3(link::TPB), 0, stream, d_P, n, d_F);
 	return hipGetLastError();
 }
 
