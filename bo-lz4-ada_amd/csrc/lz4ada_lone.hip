@@ -10,7 +10,7 @@
 // an output over the slot makes the block DS_RETRY, and the caller's exact
 // path then gives the reference's result.
 //
-//  1. k_lone_windows -- one workgroup per 4 KiB window of the compressed
+//  1. k_lone_windows -- one workgroup per window (512 B - 4 KiB) of the compressed
 //     block.  Every byte position is parsed as if a sequence started there
 //     (Decompress_Sequence's shape rules, lz4ada.adb:737-777), giving the
 //     position after it and its output bytes; pointer jumping in LDS then
