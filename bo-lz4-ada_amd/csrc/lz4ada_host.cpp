@@ -2385,36 +2385,10 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
 		uint32_t ctr[2] = { 0, 0 };
 		uint8_t* F = nullptr;
-		// dense resolution: a word per output byte (default); sparse: only the
-		// history-derived bytes are jumped
-		// (sparse, LZ4ADA_LINKED_SPARSE=1: measured slower -- three gathers per
-		// target instead of one word -- DESIGN §7)
-		static const bool dense = [] {
-			const char* e = getenv("LZ4ADA_LINKED_SPARSE");
-			return !(e && e[0] == '1');
-		}();
-		if (!dense) {
-			F = sink.dst(n);
-			struct {
-				uint8_t* p;
-			} d_U{ F ? scratch(SC_U, size_t(std::max<int64_t>(n, 1)) + 64) : nullptr };
-			if (!d_U.p)
-				return BULK_EXACT;
-			HIP_OK(launch_link_init2(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, d_U.p, F,
-			                         d_ctr.p, stream));
-			d2h(ctr, d_ctr.p, sizeof ctr, stream);
-			phase("init2");
-			for (int round = 0; ctr[0] > 0; ++round) {
-				if (round > 64)
-					return BULK_EXACT;  // never expected: every pointer goes strictly back
-				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
-				HIP_OK(launch_link_jump2(d_P.p, d_U.p, F, n, d_tail[cur].p, tail_valid, d_ctr.p, stream));
-				d2h(ctr, d_ctr.p, sizeof ctr, stream);
-				if (ctr[1])
-					return BULK_EXACT;  // a reference before the frame start: the exact error
-			}
-			phase("jumps2");
-		} else {
+		// a word per output byte (resolving only the history-derived bytes,
+		// round 4's sparse form, measured slower -- three gathers per target
+		// instead of one word -- DESIGN §7)
+		{
 			// the constant bytes go to F with the words, each round writes the
 			// bytes it resolves: the last round leaves the output
 			F = sink.dst(n);

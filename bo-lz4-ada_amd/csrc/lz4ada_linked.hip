@@ -312,141 +312,6 @@ __global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int
 }
 
 
-// Sparse resolution (round 4): only the bytes that came from history need
-// pointer jumping (14% of the bench's mixed linked frame, 46% of dense:
-// the rest are literals, copied on inside the block).  k_link_init2 writes
-// every constant byte straight to its final place F, and for each
-// history-derived byte its pointer word P[a] and a 1 in the byte map U;
-// k_link_jump2 walks U 16 positions per lane and resolves only the marked
-// ones, reading a target's byte from F when U says it is a constant and its
-// word from P otherwise, and writes F[a] when a word resolves -- no word
-// per constant byte, no emit pass, no atomics.  U is read-only after init;
-// P words change from a pointer to another pointer along the same chain or
-// to RES | byte, so a concurrent reader sees a valid word either way (as in
-// k_link_jump).  (A compacted list with one global counter per wave was
-// 4x slower than the dense form: 4M atomics on one address.)
-__global__ __launch_bounds__(TPB) void k_link_init2(const uint8_t* __restrict__ x,
-                                                    const uint8_t* __restrict__ y,
-                                                    const uint8_t* __restrict__ h,
-                                                    const lz4ada_block_desc* __restrict__ desc,
-                                                    const lz4ada_block_status* __restrict__ st,
-                                                    const int64_t* __restrict__ A, uint32_t nblocks,
-                                                    uint32_t* __restrict__ P, uint8_t* __restrict__ U,
-                                                    uint8_t* __restrict__ F, uint32_t* __restrict__ ctr)
-{
-	const uint32_t b = blockIdx.x;
-	if (b >= nblocks)
-		return;
-	const uint64_t ob = desc[b].out_off;  // 256-byte aligned slot
-	const int64_t len = st[b].out_len;
-	const int64_t ab = A[b];
-	uint32_t unres = 0;
-	for (int64_t q0 = 4 * (int64_t(blockIdx.y) * TPB + threadIdx.x); q0 < len;
-	     q0 += 4 * int64_t(gridDim.y) * TPB) {
-		const uint32_t wx = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(x) + ob + q0);
-		const uint32_t wy = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(y) + ob + q0);
-		const uint32_t wh = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(h) + ob + q0);
-		uint32_t fl = 0;  // byte i: 1 if history-derived
-		const int64_t a = ab + q0;
-#pragma unroll
-		for (int i = 0; i < 4; ++i) {
-			const uint32_t bx = (wx >> (8 * i)) & 255u, by = (wy >> (8 * i)) & 255u;
-			const uint32_t bh = (wh >> (8 * i)) & 255u;
-			if (q0 + i < len && bx != by) {
-				fl |= 1u << (8 * i);
-				P[a + i] = uint32_t(ab + int64_t(bx | (bh << 8)));
-				++unres;
-			}
-		}
-		GLOBAL uint8_t* f = gptr(F) + a;
-		GLOBAL uint8_t* u = gptr(U) + a;
-		if (q0 + 4 <= len && (a & 3) == 0) {
-			*reinterpret_cast<GLOBAL uint32_t*>(u) = fl;
-			if (fl == 0) {
-				*reinterpret_cast<GLOBAL uint32_t*>(f) = wx;
-			} else {
-#pragma unroll
-				for (int i = 0; i < 4; ++i)
-					if (!(fl >> (8 * i) & 1u))
-						f[i] = uint8_t(wx >> (8 * i));
-			}
-		} else {
-#pragma unroll
-			for (int i = 0; i < 4; ++i)
-				if (q0 + i < len) {
-					u[i] = uint8_t(fl >> (8 * i));
-					if (!(fl >> (8 * i) & 1u))
-						f[i] = uint8_t(wx >> (8 * i));
-				}
-		}
-	}
-	wave_count(ctr, unres);
-}
-
-// One pointer-jumping round over the marked positions of U[0, n), four
-// positions per lane: the marks and words of all four, then every target's
-// mark, byte and word, are loaded together before any is used (one
-// dependent round trip per level, not one per position).  ctr[0]: words
-// still unresolved after the round; ctr[1]: references before the frame
-// start.
-__global__ __launch_bounds__(TPB) void k_link_jump2(uint32_t* __restrict__ P, const uint8_t* __restrict__ U,
-                                                    uint8_t* __restrict__ F, int64_t n,
-                                                    const uint8_t* __restrict__ tail,
-                                                    int64_t tail_valid, uint32_t* __restrict__ ctr)
-{
-	uint32_t unres = 0, bad = 0;
-	GLOBAL uint32_t* Pg = gptr(P);
-	for (int64_t a0 = 4 * (int64_t(blockIdx.x) * TPB + threadIdx.x); a0 < n;
-	     a0 += 4 * int64_t(gridDim.x) * TPB) {
-		uint32_t um;
-		if (a0 + 4 <= n) {
-			um = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(U) + a0);
-		} else {
-			um = 0;
-			for (int64_t i = a0; i < n; ++i)
-				um |= uint32_t(U[i]) << (8 * (i - a0));
-		}
-		if (um == 0)
-			continue;
-		uint32_t w[4];
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-			w[i] = (um >> (8 * i) & 1u) ? Pg[a0 + i] : RES;
-		int64_t t[4];
-		uint32_t tu[4], tf[4], tp[4];
-#pragma unroll
-		for (int i = 0; i < 4; ++i) {
-			t[i] = (w[i] & RES) ? 0 : int64_t(w[i]) - HISTORY_SIZE;
-			const int64_t tc = t[i] < 0 ? 0 : t[i];
-			tu[i] = (w[i] & RES) || t[i] < 0 ? 0u : uint32_t(U[tc]);
-			tf[i] = (w[i] & RES) || t[i] < 0 ? 0u : uint32_t(F[tc]);
-			tp[i] = (w[i] & RES) || t[i] < 0 ? RES : Pg[tc];
-		}
-#pragma unroll
-		for (int i = 0; i < 4; ++i) {
-			if (w[i] & RES)
-				continue;
-			uint32_t f;
-			if (t[i] < 0) {
-				if (t[i] < -tail_valid) {
-					++bad;
-					continue;
-				}
-				f = RES | tail[HISTORY_SIZE + t[i]];
-			} else {
-				f = tu[i] ? tp[i] : (RES | tf[i]);  // a constant is final since k_link_init2
-			}
-			Pg[a0 + i] = f;
-			if (f & RES)
-				F[a0 + i] = uint8_t(f);
-			else
-				++unres;
-		}
-	}
-	wave_count(&ctr[0], unres);
-	wave_count(&ctr[1], bad);
-}
-
 // tail_new = the last 65536 bytes of (tail_old ++ F[0, n)).
 __global__ __launch_bounds__(TPB) void k_link_tail(const uint8_t* __restrict__ F, int64_t n,
                                                    const uint8_t* __restrict__ tail_old,
@@ -504,30 +369,6 @@ hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int
 		return hipSuccess;
 	hipLaunchKernelGGL(link::k_link_jump, dim3(grid_for(n, 4)), dim3(link::TPB), 0, stream, d_P, n, d_tail,
 	                   tail_valid, d_F, d_act_in, d_act_out, d_ctr);
-	return hipGetLastError();
-}
-
-hipError_t launch_link_init2(const uint8_t* x, const uint8_t* y, const uint8_t* h,
-                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
-                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                             uint8_t* d_U, uint8_t* d_F, uint32_t* d_ctr, hipStream_t stream)
-{
-	if (nblocks == 0)
-		return hipSuccess;
-	const int64_t per = 16 * 4 * link::TPB;
-	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
-	hipLaunchKernelGGL(link::k_link_init2, dim3(nblocks, gy), dim3(link::TPB), 0, stream, x, y, h, d_desc,
-	                   d_st, d_A, nblocks, d_P, d_U, d_F, d_ctr);
-	return hipGetLastError();
-}
-
-hipError_t launch_link_jump2(uint32_t* d_P, const uint8_t* d_U, uint8_t* d_F, int64_t n,
-                             const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_ctr, hipStream_t stream)
-{
-	if (n <= 0)
-		return hipSuccess;
-	hipLaunchKernelGGL(link::k_link_jump2, dim3(grid_for(n, 4)), dim3(link::TPB), 0, stream, d_P, d_U, d_F,
-	                   n, d_tail, tail_valid, d_ctr);
 	return hipGetLastError();
 }
 
