@@ -2394,23 +2394,17 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			F = sink.dst(n);
 			if (!F)
 				return BULK_EXACT;
-			// span activity flags, double-buffered across rounds; with the
-			// init-time step forward (LZ4ADA_LINK_FWD=1) init writes the first
-			// round's flags.  Off by default (tools/r04_linked.sh, 1 GiB of
-			// 256 KiB blocks: mixed 10.32 vs 10.35 ms, chain 13.5 vs 15.4,
-			// dense 31.0 vs 23.7 -- its byte gathers cost what the round saves)
-			static const bool fwd = [] {
-				const char* e = getenv("LZ4ADA_LINK_FWD");
-				return e && e[0] == '1';
-			}();
+			// span activity flags, double-buffered across rounds (an init that
+			// also stepped every history-derived byte one pointer forward was
+			// measured and dropped: mixed 10.32 vs 10.35 ms, chain 13.5 vs
+			// 15.4, dense 31.0 vs 23.7 -- its byte gathers cost what the round
+			// saves)
 			const int64_t ns = link_spans(n);
 			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
 			if (!act)
 				return BULK_EXACT;
-			if (fwd)
-				HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
 			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
-			                        d_tail[cur].p, tail_valid, fwd ? act + ns : nullptr, d_ctr.p, stream));
+			                        d_ctr.p, stream));
 			d2h(ctr, d_ctr.p, sizeof ctr, stream);
 			phase("init");
 			for (int round = 0; ctr[0] > 0; ++round) {
@@ -2418,7 +2412,7 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 					return BULK_EXACT;  // never expected: every pointer goes strictly back
 				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
 				uint8_t* a_out = act + (round & 1) * ns;
-				const uint8_t* a_in = (round || fwd) ? act + ((round + 1) & 1) * ns : nullptr;
+				const uint8_t* a_in = round ? act + ((round + 1) & 1) * ns : nullptr;
 				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out, d_ctr.p,
 				                        stream));
 				d2h(ctr, d_ctr.p, sizeof ctr, stream);

@@ -112,29 +112,6 @@ __device__ __forceinline__ void f_store16(uint8_t* F, int64_t a, uint32_t o0, ui
 // per lane: dwordx4 loads of the three copies, four 16-byte word stores.
 constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
 
-// One step along a history-derived byte's pointer at init time: the word of
-// batch position t (the byte it copies) from the three decodes themselves --
-// a constant there resolves the byte now, a history-derived one gives the
-// next pointer.  Positions before the batch come from the tail.  b: the
-// copying byte's block (t lies in an earlier one).
-__device__ __forceinline__ uint32_t link_forward(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
-                                                 const uint8_t* __restrict__ h,
-                                                 const lz4ada_block_desc* __restrict__ desc,
-                                                 const int64_t* __restrict__ A, uint32_t b, int64_t t,
-                                                 const uint8_t* __restrict__ tail, int64_t tail_valid)
-{
-	if (t < 0)
-		return t >= -tail_valid ? (RES | tail[HISTORY_SIZE + t]) : uint32_t(t + HISTORY_SIZE);
-	uint32_t c = b;
-	while (c > 0 && A[c] > t)
-		--c;
-	const uint64_t o = desc[c].out_off + uint64_t(t - A[c]);
-	const uint32_t bx = x[o], by = y[o];
-	if (bx == by)
-		return RES | bx;
-	return uint32_t(A[c] + int64_t(bx | (uint32_t(h[o]) << 8)));
-}
-
 __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x,
                                                    const uint8_t* __restrict__ y,
                                                    const uint8_t* __restrict__ h,
@@ -142,8 +119,7 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
                                                    const lz4ada_block_status* __restrict__ st,
                                                    const int64_t* __restrict__ A, uint32_t nblocks,
                                                    uint32_t* __restrict__ P, uint8_t* __restrict__ F,
-                                                   const uint8_t* __restrict__ tail, int64_t tail_valid,
-                                                   uint8_t* __restrict__ act, uint32_t* __restrict__ ctr)
+                                                   uint32_t* __restrict__ ctr)
 {
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
@@ -159,34 +135,21 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 		const u32x4 vh = *reinterpret_cast<const GLOBAL u32x4*>(gptr(h) + ob + q0);
 		const uint32_t wx[4] = { vx.x, vx.y, vx.z, vx.w }, wy[4] = { vy.x, vy.y, vy.z, vy.w },
 		               wh[4] = { vh.x, vh.y, vh.z, vh.w };
+		// branch-free per byte (a select per byte kept the compiler from
+		// making sixteen exec-masked regions of the loop body); positions fit
+		// 31 bits (bulk_linked checks), so the words are 32-bit sums
+		const int32_t nv = int32_t(min<int64_t>(16, len - q0));
+		const uint32_t hb = uint32_t(ab);  // + k: history position k's source, encoded + 65536
 		uint32_t v[16];
 #pragma unroll
 		for (int i = 0; i < 16; ++i) {
 			const uint32_t bx = (wx[i >> 2] >> (8 * (i & 3))) & 255u;
 			const uint32_t by = (wy[i >> 2] >> (8 * (i & 3))) & 255u;
 			const uint32_t bh = (wh[i >> 2] >> (8 * (i & 3))) & 255u;
-			const bool from_hist = bx != by && q0 + i < len;
-			// history position k = bx | bh << 8 is byte k - 65536 of the
-			// block-relative output: source ab + k - 65536, encoded + 65536
-			v[i] = from_hist ? uint32_t(ab + int64_t(bx | (bh << 8))) : (RES | bx);
-		}
-		if (act) {  // one step forward now (act: flags for the first jump round)
-			uint32_t u = 0;
-#pragma unroll
-			for (int i = 0; i < 16; ++i) {
-				if (!(v[i] & RES))
-					v[i] = link_forward(x, y, h, desc, A, b, int64_t(v[i]) - HISTORY_SIZE, tail, tail_valid);
-				u += (v[i] & RES) ? 0u : 1u;
-			}
-			if (u) {
-				act[(ab + q0) / SPAN] = 1;
-				act[(ab + q0 + 15) / SPAN] = 1;
-			}
-			unres += u;
-		} else {
-#pragma unroll
-			for (int i = 0; i < 16; ++i)
-				unres += (v[i] & RES) ? 0u : 1u;
+			const uint32_t hist = (bx != by && i < nv) ? 0xFFFFFFFFu : 0u;
+			const uint32_t lit = RES | bx, ptr = hb + (bx | (bh << 8));
+			v[i] = lit ^ ((lit ^ ptr) & hist);
+			unres += hist & 1u;
 		}
 		GLOBAL uint32_t* dst = gptr(P) + ab + q0;
 		if (((ab & 3) == 0) && q0 + 16 <= len) {
@@ -339,8 +302,7 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                            uint8_t* d_F, const uint8_t* d_tail, int64_t tail_valid, uint8_t* d_act,
-                            uint32_t* d_ctr, hipStream_t stream)
+                            uint8_t* d_F, uint32_t* d_ctr, hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
@@ -349,7 +311,7 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h
 	const int64_t per = 4 * 16 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
 	hipLaunchKernelGGL(link::k_link_init, dim3(nblocks, gy), dim3(link::TPB), 0, stream, x, y, h, d_desc,
-	                   d_st, d_A, nblocks, d_P, d_F, d_tail, tail_valid, d_act, d_ctr);
+	                   d_st, d_A, nblocks, d_P, d_F, d_ctr);
 	return hipGetLastError();
 }
 

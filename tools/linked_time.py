@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """configs[4]'s linked row alone (bench.bench_linked: 4096 x 256 KiB mixed
-blocks, device-resident), for A/B of the linked resolution (LZ4ADA_LINK_FWD=1:
-init steps every history-derived byte one pointer forward) and phase times
-(LZ4ADA_TRACE_LINKED=1 prints them to stderr)."""
+blocks, device-resident) and its phase times (LZ4ADA_TRACE_LINKED=1 prints
+them to stderr)."""
 import json
 import os
 import sys
@@ -24,5 +23,4 @@ if __name__ == "__main__":
     st = torch.cuda.current_stream(dev)
     kind = sys.argv[1] if len(sys.argv) > 1 else "mixed"
     r = bench.bench_linked((lz4ada, lz4frame, xxhash, torch), dev, st.cuda_stream, st, kind=kind)
-    print(json.dumps({k: r[k] for k in ("decode_ms", "MiB_s", "frac")}),
-          "fwd" if os.environ.get("LZ4ADA_LINK_FWD") == "1" else "dense", kind, flush=True)
+    print(json.dumps({k: r[k] for k in ("decode_ms", "MiB_s", "frac")}), kind, flush=True)
