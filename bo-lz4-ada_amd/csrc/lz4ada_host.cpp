@@ -2403,8 +2403,11 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
 			if (!act)
 				return BULK_EXACT;
+			// init flags the spans that hold a history-derived byte: the
+			// first round reads only those
+			HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
 			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
-			                        d_ctr.p, stream));
+			                        act + ns, d_ctr.p, stream));
 			d2h(ctr, d_ctr.p, sizeof ctr, stream);
 			phase("init");
 			for (int round = 0; ctr[0] > 0; ++round) {
@@ -2412,7 +2415,7 @@ static BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_
 					return BULK_EXACT;  // never expected: every pointer goes strictly back
 				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
 				uint8_t* a_out = act + (round & 1) * ns;
-				const uint8_t* a_in = round ? act + ((round + 1) & 1) * ns : nullptr;
+				const uint8_t* a_in = act + ((round + 1) & 1) * ns;
 				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out, d_ctr.p,
 				                        stream));
 				d2h(ctr, d_ctr.p, sizeof ctr, stream);

@@ -164,7 +164,7 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                            uint8_t* d_F, uint32_t* d_ctr, hipStream_t stream);
+                            uint8_t* d_F, uint8_t* d_act, uint32_t* d_ctr, hipStream_t stream);
 // One pointer-jumping round; d_act_in (nullptr: every span) / d_act_out:
 // a byte per span of positions, 1 while the span holds an unresolved word.
 int64_t link_spans(int64_t n);

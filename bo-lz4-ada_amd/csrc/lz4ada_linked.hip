@@ -119,7 +119,7 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
                                                    const lz4ada_block_status* __restrict__ st,
                                                    const int64_t* __restrict__ A, uint32_t nblocks,
                                                    uint32_t* __restrict__ P, uint8_t* __restrict__ F,
-                                                   uint32_t* __restrict__ ctr)
+                                                   uint8_t* __restrict__ act, uint32_t* __restrict__ ctr)
 {
 	const uint32_t b = blockIdx.x;
 	if (b >= nblocks)
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 		// 31 bits (bulk_linked checks), so the words are 32-bit sums
 		const int32_t nv = int32_t(min<int64_t>(16, len - q0));
 		const uint32_t hb = uint32_t(ab);  // + k: history position k's source, encoded + 65536
-		uint32_t v[16];
+		uint32_t v[16], u = 0;
 #pragma unroll
 		for (int i = 0; i < 16; ++i) {
 			const uint32_t bx = (wx[i >> 2] >> (8 * (i & 3))) & 255u;
@@ -149,8 +149,13 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 			const uint32_t hist = (bx != by && i < nv) ? 0xFFFFFFFFu : 0u;
 			const uint32_t lit = RES | bx, ptr = hb + (bx | (bh << 8));
 			v[i] = lit ^ ((lit ^ ptr) & hist);
-			unres += hist & 1u;
+			u += hist & 1u;
 		}
+		if (u) {  // the first jump round visits only the spans flagged here
+			act[(ab + q0) / SPAN] = 1;
+			act[(ab + q0 + 15) / SPAN] = 1;
+		}
+		unres += u;
 		GLOBAL uint32_t* dst = gptr(P) + ab + q0;
 		if (((ab & 3) == 0) && q0 + 16 <= len) {
 #pragma unroll
@@ -302,7 +307,7 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                            uint8_t* d_F, uint32_t* d_ctr, hipStream_t stream)
+                            uint8_t* d_F, uint8_t* d_act, uint32_t* d_ctr, hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
@@ -311,7 +316,7 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h
 	const int64_t per = 4 * 16 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
 	hipLaunchKernelGGL(link::k_link_init, dim3(nblocks, gy), dim3(link::TPB), 0, stream, x, y, h, d_desc,
-	                   d_st, d_A, nblocks, d_P, d_F, d_ctr);
+	                   d_st, d_A, nblocks, d_P, d_F, d_act, d_ctr);
 	return hipGetLastError();
 }
 
