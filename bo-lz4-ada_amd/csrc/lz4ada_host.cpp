@@ -686,6 +686,7 @@ struct lz4ada_decompressor {
 			next = 0;
 		}
 	} ahead;
+	int64_t linked_cap = int64_t(512) << 20;  // input bytes of a linked read-ahead batch
 
 	lz4ada_decompressor() { lz4ada_xxh32_reset(&hash_all, 0); }
 	~lz4ada_decompressor()
@@ -1223,7 +1224,7 @@ struct lz4ada_decompressor {
 		add(0, total - bcl, !m.is_compressed);
 		int64_t pos = total;
 		while (pos + BLOCK_SIZE_BYTES <= avail && ahead.descs.size() < max_blocks &&
-		       pos < (int64_t(512) << 20)) {
+		       pos < (linked ? linked_cap : (int64_t(512) << 20))) {
 			uint32_t w = load32(blk + pos);
 			bool stored = false;
 			if (m.is_format == F_MODERN) {
@@ -1309,6 +1310,18 @@ struct lz4ada_decompressor {
 		if (r != BULK_OK && r != BULK_FAIL_AT) {
 			ahead.clear();
 			return false;  // each block alone (lone decoder with history, else exact)
+		}
+		// A batch that stops early (quirk D1, an error) is decoded again from
+		// the failing block on: the next batch is kept to about twice what this
+		// one served, so frames with many such blocks are not re-decoded to
+		// the end each time; a clean batch lets it grow back.
+		if (r == BULK_OK) {
+			linked_cap = std::min<int64_t>(int64_t(512) << 20, 2 * linked_cap);
+		} else {
+			int64_t served = 0;
+			for (size_t k = 0; k < lens.size() && k < nb; ++k)
+				served += int64_t(ahead.descs[k].in_len) + BLOCK_SIZE_BYTES + m.block_checksum_length;
+			linked_cap = std::max<int64_t>(int64_t(1) << 20, 2 * served);
 		}
 		uint64_t off = 0;
 		for (size_t k = 0; k < nb; ++k) {
