@@ -1106,7 +1106,7 @@ struct lz4ada_decompressor {
 		HIP_OK(launch_decode_lone_parse(d_blk.p, raw_len, cap, d_bst.p, d_lone.p, sb, stream,
 		                                linked ? d_buf.p + output_pos_history - n0 : nullptr, int32_t(n0),
 		                                linked ? d_buf.p : nullptr, int32_t(n1),
-		                                linked && d1_window() ? 1 : 0));
+		                                linked && d1_window() ? int(output_pos_history) : 0));
 		if (bcl > 0) {
 			const auto c = block_checksum(blk, blen);
 			if (!c.first) {

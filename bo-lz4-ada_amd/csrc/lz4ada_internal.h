@@ -180,13 +180,16 @@ hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail
 // lone_scratch_bytes(n, cap) bytes.  History (a linked frame's block): the
 // n0 + n1 <= 65535 bytes before the block, h0 then h1 (device memory; the
 // reference's Buffer keeps them in two places), readable by its matches;
-// d1_guard: a match reaching >= D1_OFF back before the block start declines
-// it (quirk D1).  Without history such a match declines it.
+// d1: 0; 1 -- a match reaching >= D1_OFF back before the block start
+// declines it (quirk D1); or the round's Output_Pos_History (>= 65536) --
+// the block follows a round that ended there, and quirk D1's overshoot
+// bytes are emulated (lz4ada_lone.hip).  Without history such a match
+// declines it.
 int64_t lone_scratch_bytes(int64_t n, int64_t cap);
 hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
                               lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
                               hipStream_t stream, const uint8_t* d_h0 = nullptr, int32_t n0 = 0,
-                              const uint8_t* d_h1 = nullptr, int32_t n1 = 0, int d1_guard = 0);
+                              const uint8_t* d_h1 = nullptr, int32_t n1 = 0, int d1 = 0);
 // The same in two halves: the parse (steps 1-3: nothing written to d_out,
 // the status set to DS_RETRY on a decline) and the emit (step 4: the bytes
 // to d_out when the status is still OK).  A caller may check something on
@@ -194,7 +197,7 @@ hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, i
 hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap,
                                     lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
                                     hipStream_t stream, const uint8_t* d_h0, int32_t n0,
-                                    const uint8_t* d_h1, int32_t n1, int d1_guard);
+                                    const uint8_t* d_h1, int32_t n1, int d1);
 hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ada_block_status* d_st,
                                    void* d_scratch, hipStream_t stream, int32_t H);
 

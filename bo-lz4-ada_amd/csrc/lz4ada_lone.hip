@@ -470,8 +470,25 @@ struct SeqRec {
 	uint32_t o;    // first output byte, from the window's first
 	int32_t lit;   // block position of the first literal
 	int32_t L;     // literal bytes
-	uint32_t off;  // match offset (0: none)
+	uint32_t off;  // match offset (0: none) | k1 << 16 (quirk D1, below)
+	int32_t ml;    // match bytes
 };
+
+// Quirk D1 (lz4ada.adb:790-824, 845-904), emulated.  Right after a round
+// that ended at Output_Pos_History = OPH in [65536, 65542], the new round
+// writes from Buffer position 0 and a history match at output position p
+// reads Buffer(p - off + OPH ...) = Buffer(p + d ...), d = OPH - off.  The
+// reference's wild copies leave up to 7 bytes past the write frontier:
+// after this sequence's literal Write_Output (Data = the block payload, 8
+// bytes a chunk while 8 payload bytes remain), Buffer(p .. p + ovs - 1)
+// holds the payload bytes right after the literals, ovs = 8 ceil(L / 8) - L
+// (every older write ended before p - L, its overshoot before p).  So the
+// match's first k1 = ovs - d bytes (d < ovs) are those payload bytes -- lit
+// + L + d + j -- and the rest are history; its own chunks read ahead of
+// what they write.  Declined (exact path) instead: no literals (the last
+// write was a match, whose overshoot is a Buffer source), a literal run
+// whose last chunk was not wild (the payload's last 8 bytes), a match that
+// also reads the current round (p + ml > off).
 
 template <int32_t LW>
 __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ blk, int32_t n,
@@ -481,8 +498,11 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
                                                    LoneCtl* __restrict__ ctl,
                                                    lz4ada_block_status* __restrict__ st,
                                                    uint32_t* __restrict__ Wbase, int32_t H,
-                                                   int32_t d1_guard)
+                                                   int32_t d1, int32_t n1)
 {
+	// d1: 0, or 1 (decline every match >= D1_OFF back before the block), or
+	// the round's OPH (>= 65536: emulate quirk D1); n1: the block's position
+	// in the round (its history's current-round part)
 	// words [0, H): the history (literals); output byte x is word H + x
 	constexpr int32_t LP = LW / LT, LSTG = 2 * LW;
 	constexpr int32_t MAXSEQ = LW / 3 + 2;  // chain sequences starting in a window (>= 3 bytes but the last)
@@ -490,7 +510,7 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 	__shared__ alignas(16) uint8_t s[LSTG + 32];
 	__shared__ uint16_t J[LW];
 	__shared__ uint8_t mark[LW];
-	__shared__ alignas(16) SeqRec R[MAXSEQ + 1];
+	__shared__ SeqRec R[MAXSEQ + 1];
 	__shared__ uint16_t T16[OT];
 	__shared__ uint32_t wred[3][LT / 64];
 	if (ctl->code != DS_OK)
@@ -572,7 +592,7 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 			bad = true;  // never expected: k_lone_chain accepted this chain
 			continue;
 		}
-		R[sj] = SeqRec{ mine, q.lit, q.L, uint32_t(q.off) };
+		R[sj] = SeqRec{ mine, q.lit, q.L, uint32_t(q.off), q.ml };
 		mine += q.os;
 	}
 	const uint32_t oi = uint32_t(wave_incl_scan(int32_t(mine)));
@@ -590,10 +610,23 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 		R[j].o = o;
 		const int32_t L = R[j].L;
 		const int64_t off = int64_t(R[j].off), oa = int64_t(wo) + o;
-		if (off && oa + L + H < off)
+		if (off && oa + L + H < off) {
 			bad = true;  // a reference before the history it was given (exact path)
-		else if (d1_guard && off && oa + L < off && off >= D1_OFF)
-			bad = true;  // quirk D1: the reference's wild copy may have clobbered it
+		} else if (d1 == 1 && off && oa + L < off && off >= D1_OFF) {
+			bad = true;  // quirk D1 (not emulated by this caller)
+		} else if (d1 > 1 && off && n1 + oa + L < off && int64_t(d1) - off < 8) {
+			// quirk D1: a read before the round start, which may see what the
+			// literals' wild copy left
+			const int32_t d = d1 - int32_t(off);
+			const int32_t c_last = R[j].lit + 8 * ((L - 1) / 8);  // the literal copy's last chunk
+			const int32_t ovs = 8 * ((L + 7) / 8) - L;
+			if (L == 0 || c_last + 8 > n || n1 + oa + L + R[j].ml > off) {
+				bad = true;  // the cases not emulated: the exact path
+			} else if (d < ovs) {
+				const int32_t k1 = min(ovs - d, R[j].ml);
+				R[j].off = uint32_t(off) | (uint32_t(k1) << 16);
+			}
+		}
 	}
 	if (__syncthreads_or(bad)) {
 		if (tid == 0) {
@@ -647,7 +680,16 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 				const SeqRec r = R[T16[i]];
 				const uint32_t x = tb + i - r.o;
 				const uint32_t oa = wo + tb + i;
-				W[oa] = int32_t(x) < r.L ? (LIT | S.at(r.lit + int32_t(x))) : uint32_t(H) + oa - r.off;
+				const uint32_t off = r.off & 0xFFFFu, k1 = r.off >> 16;
+				const int32_t j = int32_t(x) - r.L;  // match byte
+				uint32_t v;
+				if (j < 0)
+					v = LIT | S.at(r.lit + int32_t(x));
+				else if (uint32_t(j) < k1)  // quirk D1: the literals' overshoot
+					v = LIT | S.at(r.lit + r.L + (d1 - int32_t(off)) + j);
+				else
+					v = uint32_t(H) + oa - off;
+				W[oa] = v;
 			}
 		}
 		__syncthreads();
@@ -799,7 +841,7 @@ struct LoneLayout {
 template <int32_t LW>
 static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ada_block_status* d_st,
                              uint8_t* sc, hipStream_t stream, const uint8_t* d_h0, int32_t n0,
-                             const uint8_t* d_h1, int32_t n1, int d1_guard)
+                             const uint8_t* d_h1, int32_t n1, int d1)
 {
 	constexpr int32_t CK = (int32_t(16) << 20) / LW / CT;
 	const int64_t nwin = (n + LW - 1) / LW;
@@ -829,24 +871,24 @@ static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ad
 			return err;
 	}
 	hipLaunchKernelGGL(k_lone_words<LW>, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
-	                   nxt_tab, entry, obase, ctl, d_st, W, H, d1_guard);
+	                   nxt_tab, entry, obase, ctl, d_st, W, H, d1, n1);
 	return hipGetLastError();
 }
 
 hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap,
                                     lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
                                     hipStream_t stream, const uint8_t* d_h0, int32_t n0,
-                                    const uint8_t* d_h1, int32_t n1, int d1_guard)
+                                    const uint8_t* d_h1, int32_t n1, int d1)
 {
 	if (n <= 0 || n > (int64_t(1) << 30) || cap <= 0 || cap > (int64_t(1) << 30) ||
 	    scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 || n0 + n1 > 65535)
 		return hipErrorInvalidValue;
 	uint8_t* sc = static_cast<uint8_t*>(d_scratch);
 	switch (lone_window(n)) {
-	case 512: return lone_steps<512>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
-	case 1024: return lone_steps<1024>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
-	case 2048: return lone_steps<2048>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
-	default: return lone_steps<4096>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1_guard);
+	case 512: return lone_steps<512>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
+	case 1024: return lone_steps<1024>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
+	case 2048: return lone_steps<2048>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
+	default: return lone_steps<4096>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
 	}
 }
 
@@ -864,10 +906,10 @@ hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ad
 hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
                               lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
                               hipStream_t stream, const uint8_t* d_h0, int32_t n0, const uint8_t* d_h1,
-                              int32_t n1, int d1_guard)
+                              int32_t n1, int d1)
 {
 	const hipError_t err = launch_decode_lone_parse(d_blk, n, cap, d_st, d_scratch, scratch_bytes, stream,
-	                                                d_h0, n0, d_h1, n1, d1_guard);
+	                                                d_h0, n0, d_h1, n1, d1);
 	if (err != hipSuccess)
 		return err;
 	return launch_decode_lone_emit(n, d_out, cap, d_st, d_scratch, stream, n0 + n1);

@@ -273,14 +273,45 @@ def test_facade_linked_frame_on_gpu(kind, bmax, feed):
         assert exact == 0, exact
 
 
-def test_facade_linked_d1_block_goes_exact():
-    """The hand-built D1 frame (tests/test_gpu_linked.py): the second block
-    reads history the reference's wild copy clobbered; the facade sends it
-    to the exact path and returns the reference's bytes."""
+def d1_frame(lit_len, off, tail=b"vwxyz"):
+    """A 64 KiB block, then one sequence of lit_len literals and a 10-byte
+    match `off` back (history), then a literal tail: quirk D1's shape."""
     import struct
     comp0, raw0 = lz4ada.gen_block(1, 1234, 65536)
-    lits = bytes(range(65, 85))
-    comp1 = bytes([0xF6, 20 - 15]) + lits + struct.pack("<H", 65533) + bytes([0x50]) + b"vwxyz"
+    lits = bytes(range(65, 65 + lit_len))
+    tok = (min(lit_len, 15) << 4) | 6
+    ext = bytes([lit_len - 15]) if lit_len >= 15 else b""
+    comp1 = bytes([tok]) + ext + lits + struct.pack("<H", off) + bytes([len(tail) << 4]) + tail
+    frame, _ = lz4frame.build_frame([(comp0, raw0, False), (comp1, b"", False)], 64 * KiB,
+                                    indep=False)
+    return frame
+
+
+@pytest.mark.parametrize("lit_len,off", [(20, 65533), (1, 65535), (2, 65534), (3, 65530), (7, 65529),
+                                         (13, 65534), (16, 65532), (5, 65528), (23, 65535)])
+def test_facade_linked_d1_block_on_gpu(lit_len, off):
+    """Quirk D1 (a match >= 65,529 back right after a round that ended at
+    65,536): the reference's wild copy of the literals leaves the payload
+    bytes after them in the Buffer, and the match reads some of them
+    instead of history.  The lone decoder emulates that overshoot, so the
+    block stays on the GPU and returns the reference's (corrupted) bytes."""
+    frame = d1_frame(lit_len, off)
+    for feed in (0, 4096):
+        ours, exact = trace_ours_ctx(frame, feed)
+        assert ours == trace_oracle(frame, feed)
+        assert exact == 0, exact
+
+
+def test_facade_linked_d1_without_literals_goes_exact():
+    """Quirk D1 after a match rather than literals (the last write's
+    overshoot comes from the Buffer): not emulated -- the exact path, the
+    reference's bytes."""
+    import struct
+    comp0, raw0 = lz4ada.gen_block(1, 1234, 65536)
+    # 8 literals + a short match, then a sequence with no literals whose
+    # match reaches 65,533 back
+    comp1 = (bytes([0x81]) + b"ABCDEFGH" + struct.pack("<H", 3) + bytes([0x06]) +
+             struct.pack("<H", 65533) + bytes([0x50]) + b"vwxyz")
     frame, _ = lz4frame.build_frame([(comp0, raw0, False), (comp1, b"", False)], 64 * KiB,
                                     indep=False)
     for feed in (0, 4096):
