@@ -251,6 +251,12 @@ struct PinBuf {
 		bytes = b.second;
 		n = count;
 	}
+	void swap(PinBuf& o)
+	{
+		std::swap(p, o.p);
+		std::swap(n, o.n);
+		std::swap(bytes, o.bytes);
+	}
 };
 
 // The facade's streams and event, reused across contexts.
@@ -652,10 +658,13 @@ struct lz4ada_decompressor {
 	// A large block's content hash runs on a helper thread while the caller
 	// feeds the next block, over the pinned staging copy of its output (our
 	// memory, so the caller may reuse its Buffer); every reader of hash_all
-	// or writer of the staging joins it first.
+	// joins it first.  The staging ping-pongs: a block handed to the hasher
+	// leaves in stage_hashed, so the next block's copy never waits for it
+	// (the hasher runs one job at a time, and submit() joins the previous one).
 	Worker hasher;
 	void hash_wait() { hasher.wait(); }
 	PinBuf stage;  // a block's output on its way to the caller's Buffer
+	PinBuf stage_hashed;  // the staging the hasher may be reading
 	PinBuf stage_st;  // its status
 	std::vector<uint8_t> blk_tmp;  // a block assembled from cached + new input
 	DevBuf<lz4ada_xxh32_state> d_tmp_hash;
@@ -966,7 +975,6 @@ struct lz4ada_decompressor {
 			return;
 		static const bool trace = getenv("LZ4ADA_TRACE_FACADE") != nullptr;
 		const auto t0 = std::chrono::steady_clock::now();
-		hash_wait();  // the staging may still be hashed
 		stage.reserve(size_t(nout));
 		HIP_OK(hipMemcpyAsync(stage.p, d_buf.p + first, size_t(nout), hipMemcpyDeviceToHost, stream));
 		HIP_OK(hipStreamSynchronize(stream));
@@ -987,10 +995,13 @@ struct lz4ada_decompressor {
 		if (m.content_checksum_length == 0)
 			return;
 		const uint8_t* p = stage.p;
-		if (nout >= (int64_t(64) << 10))
+		if (nout >= (int64_t(64) << 10)) {
 			hasher.submit([this, p, nout] { host_xxh32_update(hash_all, p, size_t(nout)); });
-		else
+			stage.swap(stage_hashed);
+		} else {
+			hash_wait();  // the previous block's share first
 			host_xxh32_update(hash_all, p, size_t(nout));
+		}
 	}
 
 	// A lone block is latency-bound: the lone-block decoder (every step
@@ -1101,12 +1112,23 @@ struct lz4ada_decompressor {
 		int64_t n0 = 0, n1 = 0;
 		if (linked)
 			history_of(start, n0, n1);
+		static const bool trace = getenv("LZ4ADA_TRACE_FACADE") != nullptr;
+		auto t0 = std::chrono::steady_clock::now();
+		auto lap = [&](const char* name) {
+			if (!trace)
+				return;
+			const auto t1 = std::chrono::steady_clock::now();
+			fprintf(stderr, "[facade]   lone %-7s %8.3f ms\n", name,
+			        std::chrono::duration<double, std::milli>(t1 - t0).count());
+			t0 = t1;
+		};
 		const int64_t sb = lone_scratch_bytes(raw_len, cap);
 		d_lone.reserve(size_t(sb));
 		HIP_OK(launch_decode_lone_parse(d_blk.p, raw_len, cap, d_bst.p, d_lone.p, sb, stream,
 		                                linked ? d_buf.p + output_pos_history - n0 : nullptr, int32_t(n0),
 		                                linked ? d_buf.p : nullptr, int32_t(n1),
 		                                linked && d1_window() ? int(output_pos_history) : 0));
+		lap("parse");
 		if (bcl > 0) {
 			const auto c = block_checksum(blk, blen);
 			if (!c.first) {
@@ -1114,17 +1136,19 @@ struct lz4ada_decompressor {
 				raise(LZ4ADA_CHECKSUM_ERROR, c.second);
 			}
 		}
+		lap("cksum");
 		HIP_OK(launch_decode_lone_emit(raw_len, d_buf.p + start, cap, d_bst.p, d_lone.p, stream,
 		                               int32_t(n0 + n1)));
 		// the likely share of the output comes back with the status
 		const int64_t spec = std::min<int64_t>(cap, std::max<int64_t>(4 * raw_len, int64_t(64) << 10));
-		hash_wait();  // the staging may still be hashed
 		stage.reserve(size_t(cap));
 		stage_st.reserve(sizeof(lz4ada_block_status));
 		HIP_OK(hipMemcpyAsync(stage_st.p, d_bst.p, sizeof(lz4ada_block_status), hipMemcpyDeviceToHost,
 		                      stream));
 		HIP_OK(hipMemcpyAsync(stage.p, d_buf.p + start, size_t(spec), hipMemcpyDeviceToHost, stream));
+		lap("enqueue");
 		HIP_OK(hipStreamSynchronize(stream));
+		lap("wait");
 		lz4ada_block_status st;
 		memcpy(&st, stage_st.p, sizeof st);
 		if (st.code != DS_OK)
@@ -1144,6 +1168,7 @@ struct lz4ada_decompressor {
 		last = start + nout - 1;
 		if (nout > 0)
 			to_caller(buf + first, nout);
+		lap("deliver");
 		return LONE_DONE;
 	}
 
