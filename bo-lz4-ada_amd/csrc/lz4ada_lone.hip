@@ -47,7 +47,7 @@ constexpr int32_t LW_MIN = 512;
 constexpr int32_t LT = 256;               // threads per workgroup
 constexpr uint32_t NX_BAD = 0xFFFFFFFFu;  // not a sequence (or beyond what a window parses)
 constexpr uint32_t LIT = 0x80000000u;     // word: a literal byte
-constexpr int32_t RES_SLICE = 4096;       // output words per workgroup in k_lone_resolve
+constexpr int32_t RES_SLICE = 4096;       // largest output slice per workgroup in k_lone_resolve
 constexpr int32_t MAX_RUN_L = 1 << 28;
 static_assert(RES_SLICE % (4 * LT) == 0, "lone-decoder tiling");
 
@@ -710,17 +710,20 @@ __device__ __forceinline__ void w_store(uint32_t* p, uint32_t v)
 	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr int32_t RPT = RES_SLICE / LT;  // words per thread
-
+// SL output words per workgroup: a small block takes small slices, so its
+// jump rounds spread over more CUs with fewer gathers per lane each.
+template <int32_t SL>
 __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
                                                      const LoneCtl* __restrict__ ctl,
                                                      lz4ada_block_status* __restrict__ st,
                                                      uint8_t* __restrict__ out, uint32_t H)
 {
+	static_assert(SL % (4 * LT) == 0 && SL <= RES_SLICE, "lone-decoder tiling");
+	constexpr int32_t RPT = SL / LT;  // words per thread
 	if (ctl->code != DS_OK)
 		return;
 	const uint32_t total = ctl->total;
-	const uint32_t base = blockIdx.x * uint32_t(RES_SLICE);
+	const uint32_t base = blockIdx.x * uint32_t(SL);
 	if (base >= total)
 		return;
 	// thread t owns words base + 4 (t + LT k) .. +3 for k < RPT / 4: its
@@ -819,6 +822,23 @@ static int32_t lone_window(int64_t n)
 	return n <= (int64_t(1) << 20) ? 1024 : n <= (int64_t(5) << 19) ? 2048 : 4096;
 }
 
+// Resolve slice by output capacity (tools/r04_sl.sh, profiles/r04k_resolve_slice.txt:
+// lone decode of mixed / dense 64 KiB blocks 0.050 / 0.052 -> 0.042 / 0.042 ms
+// at 1024-word slices, 256 KiB 0.058 / 0.067 -> 0.052 / 0.058; 1 MiB even;
+// 4 MiB 0.171 / 0.403 -> 0.175 / 0.420, so large blocks keep 4096).
+// LZ4ADA_LONE_SLICE forces one.
+static int32_t resolve_slice(int64_t cap)
+{
+	static const int32_t forced = [] {
+		const char* e = getenv("LZ4ADA_LONE_SLICE");
+		const int v = e ? atoi(e) : 0;
+		return (v == 1024 || v == 2048 || v == 4096) ? v : 0;
+	}();
+	if (forced)
+		return forced;
+	return cap <= (int64_t(512) << 10) ? 1024 : RES_SLICE;
+}
+
 // The scratch: per-position tables, per-window entries, the control block
 // and the words (H history words, then one per output byte).
 struct LoneLayout {
@@ -897,9 +917,21 @@ hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ad
 {
 	const int64_t nwin = (n + lone_window(n) - 1) / lone_window(n);
 	const LoneLayout Lo(static_cast<uint8_t*>(d_scratch), n, nwin);
-	const uint32_t nres = uint32_t((cap + RES_SLICE - 1) / RES_SLICE);
-	hipLaunchKernelGGL(k_lone_resolve, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st, d_out,
-	                   uint32_t(H));
+	const int32_t sl = resolve_slice(cap);
+	const uint32_t nres = uint32_t((cap + sl - 1) / sl);
+	switch (sl) {
+	case 1024:
+		hipLaunchKernelGGL(k_lone_resolve<1024>, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st, d_out,
+		                   uint32_t(H));
+		break;
+	case 2048:
+		hipLaunchKernelGGL(k_lone_resolve<2048>, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st, d_out,
+		                   uint32_t(H));
+		break;
+	default:
+		hipLaunchKernelGGL(k_lone_resolve<RES_SLICE>, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st,
+		                   d_out, uint32_t(H));
+	}
 	return hipGetLastError();
 }
 
