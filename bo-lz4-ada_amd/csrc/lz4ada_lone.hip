@@ -40,7 +40,7 @@
 namespace lz4ada {
 
 // Window size LW (compressed bytes per workgroup in steps 1 and 3): 512 B
-// to 4 KiB by the block's compressed size (lone_window, host side).  Small
+// to 4 KiB by the block's compressed size and ratio (lone_window, host side).  Small
 // windows give a small block more workgroups; large ones keep the chain
 // step short where speculative chains do not merge (literal-heavy data).
 constexpr int32_t LW_MIN = 512;
@@ -804,11 +804,19 @@ int64_t lone_scratch_bytes(int64_t n, int64_t cap)
 	       4 * 65536 + 512;
 }
 
-// Window size by compressed size (tools/lone_time.py, tools/r04_lw.sh, round 4: 256 KiB mixed
-// blocks 0.129 / 0.081 / 0.059 ms at 4 / 2 / 1 KiB windows; 4 MiB mixed
-// 0.222 / 0.177 / 0.376, dense 0.362 / 0.317 / 0.289, literal 0.453 /
-// 0.580 / 0.956).  LZ4ADA_LONE_LW forces one.
-static int32_t lone_window(int64_t n)
+// Window size by compressed size n and output capacity cap
+// (tools/lone_time.py; tools/r04_lw.sh and tools/r04_lw2.sh,
+// profiles/r04m_lone_window.txt).  Literal-heavy blocks (n >= 0.9 cap) want
+// longer windows: 256 KiB 0.118 / 0.091 / 0.083 ms at 512 / 1024 / 2048,
+// 512 KiB 0.204 / 0.148 / 0.107.  Blocks with matches: 512-byte windows
+// win in isolation up to ~288 KiB compressed (256 KiB mixed / dense 0.052 /
+// 0.058 -> 0.045 / 0.051 ms), but on the facade's linked 256 KiB frame the
+// chain step's guesses stop merging at 512 and k_lone_chain's serial walk
+// goes 7 -> 24 us (tools/r04_lw3.sh, the frame 1,952 -> 1,880 MiB/s), so
+// they keep 1024 above 100 KiB.  4 MiB: mixed 0.222 / 0.177 / 0.376 ms at
+// 4 / 2 / 1 KiB, dense 0.362 / 0.317 / 0.289, literal 0.453 / 0.580 /
+// 0.956.  LZ4ADA_LONE_LW forces one.
+static int32_t lone_window(int64_t n, int64_t cap)
 {
 	static const int32_t forced = [] {
 		const char* e = getenv("LZ4ADA_LONE_LW");
@@ -819,6 +827,8 @@ static int32_t lone_window(int64_t n)
 		return forced;
 	if (n <= (int64_t(100) << 10))
 		return 512;  // 64 KiB mixed blocks 0.055 -> 0.049 ms, dense 0.061 -> 0.052 (literal 128 KiB, 130 KB: 0.068 vs 0.077)
+	if (10 * n >= 9 * cap)  // literal-heavy
+		return n <= (int64_t(192) << 10) ? 1024 : n <= (int64_t(5) << 19) ? 2048 : 4096;
 	return n <= (int64_t(1) << 20) ? 1024 : n <= (int64_t(5) << 19) ? 2048 : 4096;
 }
 
@@ -904,7 +914,7 @@ hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap
 	    scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 || n0 + n1 > 65535)
 		return hipErrorInvalidValue;
 	uint8_t* sc = static_cast<uint8_t*>(d_scratch);
-	switch (lone_window(n)) {
+	switch (lone_window(n, cap)) {
 	case 512: return lone_steps<512>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
 	case 1024: return lone_steps<1024>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
 	case 2048: return lone_steps<2048>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
@@ -915,7 +925,8 @@ hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap
 hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ada_block_status* d_st,
                                    void* d_scratch, hipStream_t stream, int32_t H)
 {
-	const int64_t nwin = (n + lone_window(n) - 1) / lone_window(n);
+	const int32_t lw = lone_window(n, cap);
+	const int64_t nwin = (n + lw - 1) / lw;
 	const LoneLayout Lo(static_cast<uint8_t*>(d_scratch), n, nwin);
 	const int32_t sl = resolve_slice(cap);
 	const uint32_t nres = uint32_t((cap + sl - 1) / sl);
