@@ -357,6 +357,7 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
 	extern __shared__ uint32_t E[];  // entries 0..nwin
 	__shared__ uint32_t wsum[CT / 64];
 	__shared__ unsigned long long total64;
+	__shared__ int32_t first_ch;  // the first window whose successor changed this pass
 	const int32_t tid = int32_t(threadIdx.x);
 	// entry w: the first chain position >= w * LW.  Guess: the exit most
 	// positions of window w-1 reach (k_lone_windows).
@@ -370,6 +371,8 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
 	uint32_t it = 0;
 	for (;;) {
 		++it;
+		if (tid == 0)
+			first_ch = INT32_MAX;
 		uint32_t nv[CK];
 #pragma unroll
 		for (int32_t k = 0; k < CK; ++k) {
@@ -383,27 +386,37 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
 		}
 		__syncthreads();
 		int ch = 0;
+		int32_t lo = INT32_MAX;  // this thread's lowest window whose successor changed
 #pragma unroll
 		for (int32_t k = 0; k < CK; ++k) {
 			const int32_t w = tid + k * CT;
 			if (w < nwin && E[w + 1] != nv[k]) {
 				E[w + 1] = nv[k];
+				lo = min(lo, w);
 				ch = 1;
 			}
 		}
+		if (ch)
+			atomicMin(&first_ch, lo);
 		if (!__syncthreads_or(ch) || it > uint32_t(nwin) + 2)
 			break;
 		// still changing after two passes: the guesses are poor (sequences
 		// too far apart for speculative chains to merge, e.g. long literal
-		// runs).  Entries 0..it are exact; one lane walks the rest, one
-		// dependent lookup per window instead of one pass per window, and
-		// the next pass confirms.
-		if (it == 2) {
+		// runs).  One lane walks the first run of wrong entries, one
+		// dependent lookup per window instead of one pass per window, up to
+		// where its entry meets the stored one (the rest of that run was
+		// already right); the next pass confirms, or finds the next run
+		// (profiles/r04o_chain_walk.txt: a linked 256 KiB frame at 512-byte
+		// windows 24 -> 11 us against walking every remaining window).
+		if (it >= 2) {
 			if (tid == 0) {
-				for (int32_t w = int32_t(it); w < nwin; ++w) {
+				for (int32_t w = first_ch; w < nwin; ++w) {
 					const uint32_t e = E[w];
 					const uint32_t lim = uint32_t(min((w + 1) * LW, n));
-					E[w + 1] = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
+					const uint32_t x = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
+					if (w > first_ch && E[w + 1] == x)
+						break;
+					E[w + 1] = x;
 				}
 			}
 			__syncthreads();
@@ -804,18 +817,14 @@ int64_t lone_scratch_bytes(int64_t n, int64_t cap)
 	       4 * 65536 + 512;
 }
 
-// Window size by compressed size n and output capacity cap
-// (tools/lone_time.py; tools/r04_lw.sh and tools/r04_lw2.sh,
-// profiles/r04m_lone_window.txt).  Literal-heavy blocks (n >= 0.9 cap) want
-// longer windows: 256 KiB 0.118 / 0.091 / 0.083 ms at 512 / 1024 / 2048,
-// 512 KiB 0.204 / 0.148 / 0.107.  Blocks with matches: 512-byte windows
-// win in isolation up to ~288 KiB compressed (256 KiB mixed / dense 0.052 /
-// 0.058 -> 0.045 / 0.051 ms), but on the facade's linked 256 KiB frame the
-// chain step's guesses stop merging at 512 and k_lone_chain's serial walk
-// goes 7 -> 24 us (tools/r04_lw3.sh, the frame 1,952 -> 1,880 MiB/s), so
-// they keep 1024 above 100 KiB.  4 MiB: mixed 0.222 / 0.177 / 0.376 ms at
-// 4 / 2 / 1 KiB, dense 0.362 / 0.317 / 0.289, literal 0.453 / 0.580 /
-// 0.956.  LZ4ADA_LONE_LW forces one.
+// Window size by compressed size n and output capacity cap, swept with
+// the first-run chain walk (tools/r04_sw.sh, profiles/r04p_window_sweep.txt;
+// earlier sweeps profiles/r04m_lone_window.txt).  Blocks with matches take
+// 512-byte windows up to ~800 KB compressed (256 KiB mixed / dense 0.045 /
+// 0.051 ms against 0.051 / 0.058 at 1 KiB) and 1 KiB above (4 MiB 0.164 /
+// 0.280 ms against 0.171 / 0.402 at 4 KiB); literal-heavy blocks (n >= 0.9
+// cap) take 1 KiB windows up to 160 KB and 2 KiB above (4 MiB 0.278 ms
+// against 0.300 at 4 KiB and 0.418 at 1 KiB).  LZ4ADA_LONE_LW forces one.
 static int32_t lone_window(int64_t n, int64_t cap)
 {
 	static const int32_t forced = [] {
@@ -825,11 +834,9 @@ static int32_t lone_window(int64_t n, int64_t cap)
 	}();
 	if (forced)
 		return forced;
-	if (n <= (int64_t(100) << 10))
-		return 512;  // 64 KiB mixed blocks 0.055 -> 0.049 ms, dense 0.061 -> 0.052 (literal 128 KiB, 130 KB: 0.068 vs 0.077)
 	if (10 * n >= 9 * cap)  // literal-heavy
-		return n <= (int64_t(192) << 10) ? 1024 : n <= (int64_t(5) << 19) ? 2048 : 4096;
-	return n <= (int64_t(1) << 20) ? 1024 : n <= (int64_t(5) << 19) ? 2048 : 4096;
+		return n <= (int64_t(160) << 10) ? 1024 : 2048;
+	return n <= (int64_t(800) << 10) ? 512 : 1024;
 }
 
 // Resolve slice by output capacity (tools/r04_sl.sh, profiles/r04k_resolve_slice.txt:
