@@ -3,7 +3,7 @@
 set -e
 cd $GRAFT_REPO_ROOT
 bash tools/r04_full.sh $1
-for sz in 262144 524288 1048576; do
+for sz in 65536 131072 262144 524288 1048576; do
   timeout -k 10 120 python tools/lone_time.py --size $sz --reps 50 --kinds mixed,dense,literal 2>&1 | grep -v amdgpu
 done
 bash tools/r04_ftr.sh $1
