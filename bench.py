@@ -397,6 +397,28 @@ def bench_c3_one_gpu(M, dev, sh, stream, recs, bmax, nblocks=C3_BLOCKS, reps=3):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / reps
     ms = sum(a.elapsed_time(b) for a, b in ev) / reps
+    # one rank's share of the same frame at N = 2 / 4 / 8 (the first
+    # 8192 / N blocks: every share holds whole periods of the 64 unique
+    # blocks, so any rank's range has the same content), through the same
+    # product call -- the per-rank compute time of the --gpus N lines, with
+    # the library's own choice of decoder for that block count
+    shares = {}
+    for n in (2, 4, 8):
+        nb = nblocks // n
+        sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(reps)]
+        lz4ada.decode_blocks_device(fp, frame_len, dp, nb, op, sp, sh)
+        for a, b in sev:
+            a.record(stream)
+            lz4ada.decode_blocks_device(fp, frame_len, dp, nb, op, sp, sh)
+            b.record(stream)
+        torch.cuda.synchronize()
+        sms = sum(a.elapsed_time(b) for a, b in sev) / reps
+        shares[f"n{n}"] = {"blocks_per_rank": nb, "kernel_ms": round(sms, 3),
+                           "decoder": lz4ada.bulk_decoder_kernel(nb),
+                           "compute_only_efficiency": round(ms / (n * sms), 4)}
+    st = check_statuses(lz4ada, d_st, nblocks // 8)
+    assert all(x.code == 0 for x in st), "c3 share: block status"
     del d_frame, d_out, d_desc, d_st, d_hash
     torch.cuda.empty_cache()
     return {"workload": f"configs[3] frame on one GPU: {nblocks} x 4 MiB independent blocks = "
@@ -406,7 +428,13 @@ def bench_c3_one_gpu(M, dev, sh, stream, recs, bmax, nblocks=C3_BLOCKS, reps=3):
             "frac": round((comp + raw) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "compressed_bytes": comp, "decoded_bytes": raw,
             "note": "same frame as the --gpus N>1 lines (strong scaling): N=1 point of the curve",
-            "golden": "per-block XXH32 of the output vs the generator"}
+            "golden": "per-block XXH32 of the output vs the generator",
+            "decoder": lz4ada.bulk_decoder_kernel(nblocks),
+            "c3_shares": shares,
+            "c3_shares_note": "one rank's shard of this frame at N=2/4/8 timed on this GPU (HIP "
+                              "events, product call); compute_only_efficiency = kernel_ms(8192) / "
+                              "(N x kernel_ms(share)): the strong-scaling ceiling before any "
+                              "communication or host-side assembly"}
 
 
 def bench_linked(M, dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024, chain=64):
@@ -473,9 +501,9 @@ def bench_linked(M, dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024
             "frac": round((comp + raw) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "compressed_bytes": comp, "decoded_bytes": raw,
             "path": "lz4ada_decode_linked_device: block checksums, k_index, 3 x k_decode_idx "
-                    "(every block at once, synthetic history X / ~X / hi), k_link_init + "
-                    "k_link_jump rounds + k_link_emit (history resolved on the GPU); wall clock "
-                    "of the whole call, device-resident frame and output",
+                    "(every block at once, synthetic history X / ~X / hi), k_link_init (words and "
+                    "bytes) + k_link_jump rounds (history resolved on the GPU); wall clock of the "
+                    "whole call, device-resident frame and output",
             "golden": "per-block XXH32 of the output vs the generator"}
 
 
@@ -671,7 +699,7 @@ def main():
     total_raw = sum(recs[i % len(recs)][2] for i in range(total_blocks))
     frame_alg = total_raw + sum(recs[i % len(recs)][1] for i in range(total_blocks))
     value = total_raw * args.steps / elapsed / MiB
-    dec_kernel = "k_decode_idx"
+    dec_kernel = lz4ada.bulk_decoder_kernel(nb)  # the kernel this block count runs
     alg_bytes = comp_bytes + raw_bytes  # compressed read once + output written once
     achieved = alg_bytes / (dec_ms * 1e-3) / 1e9
     traffic = None

@@ -111,11 +111,20 @@ static void device_check_or_raise()
 // and a dozen hipMalloc / hipHostMalloc calls per frame -- ~3.5 ms, more
 // than a 4 MiB frame of 64 KiB blocks takes to decode (tools/facade_c).
 // Blocks up to POOL_MAX bytes are kept by power-of-two size class, at most
-// POOL_KEEP bytes per kind and device; a block is pooled only after a
+// keep_limit() bytes per kind and device; a block is pooled only after a
 // device synchronisation (the implicit one of the hipFree it replaces), so
 // no queued work still uses it.  lz4ada_release_device_cache() empties them.
 struct MemPool {
-	static constexpr size_t POOL_MAX = size_t(256) << 20, POOL_KEEP = size_t(1) << 30;
+	static constexpr size_t POOL_MAX = size_t(256) << 20;
+	// idle bytes kept per pool (device / pinned): 1 GiB, or LZ4ADA_POOL_KEEP_MB
+	static size_t keep_limit()
+	{
+		static const size_t k = [] {
+			const char* e = getenv("LZ4ADA_POOL_KEEP_MB");
+			return e ? size_t(strtoull(e, nullptr, 10)) << 20 : size_t(1) << 30;
+		}();
+		return k;
+	}
 	std::mutex mu;
 	std::vector<std::tuple<int, size_t, void*>> free;  // (device, class bytes, block)
 	size_t kept = 0;
@@ -129,22 +138,30 @@ struct MemPool {
 		return c;
 	}
 	void raw_free(void* p) { (void)(pinned ? hipHostFree(p) : hipFree(p)); }
-	// -> (block, its usable bytes)
-	std::pair<void*, size_t> get(size_t bytes)
+	// A block and the device that was current when it was taken: put() syncs
+	// and files it under THAT device (a buffer released after the
+	// caller switched GPUs must not be pooled under the new one).  Pinned
+	// blocks are pooled for any device but still sync the device they served.
+	struct Block {
+		void* p;
+		size_t bytes;
+		int dev;
+	};
+	Block get(size_t bytes)
 	{
 		int dev = 0;
-		if (!pinned)
-			(void)hipGetDevice(&dev);
+		(void)hipGetDevice(&dev);
+		const int key = pinned ? 0 : dev;
 		const size_t c = bytes <= POOL_MAX ? size_class(bytes) : bytes;
 		if (c <= POOL_MAX) {
 			std::lock_guard<std::mutex> l(mu);
 			for (size_t i = 0; i < free.size(); ++i)
-				if (std::get<0>(free[i]) == dev && std::get<1>(free[i]) == c) {
+				if (std::get<0>(free[i]) == key && std::get<1>(free[i]) == c) {
 					void* p = std::get<2>(free[i]);
 					free[i] = free.back();
 					free.pop_back();
 					kept -= c;
-					return { p, c };
+					return { p, c, dev };
 				}
 		}
 		void* p = nullptr;
@@ -155,25 +172,31 @@ struct MemPool {
 			e = pinned ? hipHostMalloc(&p, c, hipHostMallocDefault) : hipMalloc(&p, c);
 		}
 		HIP_OK(e);
-		return { p, c };
+		return { p, c, dev };
 	}
-	void put(void* p, size_t c)
+	void put(void* p, size_t c, int dev)
 	{
 		if (!p)
 			return;
-		int dev = 0;
-		if (!pinned)
-			(void)hipGetDevice(&dev);
-		if (c > POOL_MAX || c != size_class(c) || hipDeviceSynchronize() != hipSuccess) {
+		// the implicit synchronisation of the hipFree this replaces, on the
+		// block's own device
+		int cur = 0;
+		(void)hipGetDevice(&cur);
+		if (cur != dev)
+			(void)hipSetDevice(dev);
+		const bool synced = hipDeviceSynchronize() == hipSuccess;
+		if (cur != dev)
+			(void)hipSetDevice(cur);
+		if (c > POOL_MAX || c != size_class(c) || !synced) {
 			raw_free(p);
 			return;
 		}
 		std::lock_guard<std::mutex> l(mu);
-		if (kept + c > POOL_KEEP) {
+		if (kept + c > keep_limit()) {
 			raw_free(p);
 			return;
 		}
-		free.emplace_back(dev, c, p);
+		free.emplace_back(pinned ? 0 : dev, c, p);
 		kept += c;
 	}
 	void release_all()
@@ -208,6 +231,7 @@ struct DevBuf {
 	T* p = nullptr;
 	size_t n = 0;      // elements
 	size_t bytes = 0;  // the block's usable bytes
+	int dev = 0;       // the device it was allocated on
 	DevBuf() = default;
 	DevBuf(const DevBuf&) = delete;
 	DevBuf& operator=(const DevBuf&) = delete;
@@ -215,7 +239,7 @@ struct DevBuf {
 	void release()
 	{
 		if (p)
-			dev_pool().put(p, bytes);
+			dev_pool().put(p, bytes, dev);
 		p = nullptr;
 		n = bytes = 0;
 	}
@@ -225,8 +249,9 @@ struct DevBuf {
 			return;
 		release();
 		const auto b = dev_pool().get(std::max<size_t>(count, 1) * sizeof(T) + 64);
-		p = static_cast<T*>(b.first);
-		bytes = b.second;
+		p = static_cast<T*>(b.p);
+		bytes = b.bytes;
+		dev = b.dev;
 		n = count;
 	}
 };
@@ -235,20 +260,22 @@ struct DevBuf {
 struct PinBuf {
 	uint8_t* p = nullptr;
 	size_t n = 0, bytes = 0;
+	int dev = 0;  // the device current when it was taken (synced on release)
 	PinBuf() = default;
 	PinBuf(const PinBuf&) = delete;
 	PinBuf& operator=(const PinBuf&) = delete;
-	~PinBuf() { pin_pool().put(p, bytes); }
+	~PinBuf() { pin_pool().put(p, bytes, dev); }
 	void reserve(size_t count)
 	{
 		if (count <= n && p)
 			return;
-		pin_pool().put(p, bytes);
+		pin_pool().put(p, bytes, dev);
 		p = nullptr;
 		n = bytes = 0;
 		const auto b = pin_pool().get(std::max<size_t>(count, 1));
-		p = static_cast<uint8_t*>(b.first);
-		bytes = b.second;
+		p = static_cast<uint8_t*>(b.p);
+		bytes = b.bytes;
+		dev = b.dev;
 		n = count;
 	}
 	void swap(PinBuf& o)
@@ -256,6 +283,7 @@ struct PinBuf {
 		std::swap(p, o.p);
 		std::swap(n, o.n);
 		std::swap(bytes, o.bytes);
+		std::swap(dev, o.dev);
 	}
 };
 
@@ -2842,11 +2870,31 @@ int lz4ada_decode_linked_device(const void* d_frame, uint64_t frame_len,
 
 int lz4ada_last_path(void) { return g_last_path; }
 
+const char* lz4ada_bulk_decoder_kernel(int64_t nblocks)
+{
+	return idx_fused_kernel_name(uint32_t(std::max<int64_t>(nblocks, 0)));
+}
+
 void lz4ada_release_device_cache(void)
 {
 	scratch_release();
 	dev_pool().release_all();
 	pin_pool().release_all();
+	// the facade's pooled streams and events too
+	std::vector<StreamSet> sets;
+	{
+		std::lock_guard<std::mutex> l(g_stream_mu);
+		sets.swap(stream_pool());
+	}
+	int cur = 0;
+	(void)hipGetDevice(&cur);
+	for (auto& x : sets) {
+		(void)hipSetDevice(x.device);
+		(void)hipStreamDestroy(x.side);
+		(void)hipEventDestroy(x.ev);
+		(void)hipStreamDestroy(x.stream);
+	}
+	(void)hipSetDevice(cur);
 }
 
 int64_t lz4ada_decoded_bound(const uint8_t* input, int64_t len)

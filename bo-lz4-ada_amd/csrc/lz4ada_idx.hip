@@ -889,6 +889,13 @@ constexpr int RMAX = MAXSEQ / 64;  // rounds of 64 sequences per batch
 constexpr int GC = 1;           // 16-byte pieces an HBM-sourced match loads in its own lane (1: fewest registers; the rest are dealt)
 constexpr int FLUSH_ST = (OW + 15) / 16 / 64 + 1;  // store instructions per flush (fixed)
 static_assert(2 * OW + 16 <= ORING, "batch + its HBM threshold must fit the ring");
+// batch cut limits (experiments: a smaller cut with the same ring and HBM threshold)
+#ifndef LZ4ADA_OW_CUT
+#define LZ4ADA_OW_CUT OW
+#endif
+#ifndef LZ4ADA_SEQ_CUT
+#define LZ4ADA_SEQ_CUT MAXSEQ
+#endif
 
 struct alignas(16) DecLds {
 	uint8_t ring[RING + 16];      // staged input: 4 chunks of 2 KiB (+ mirror)
@@ -1424,7 +1431,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		const int32_t incl = wave_incl_scan(cnt);
 		const int32_t incl_s = wave_incl_scan(nseq);
 		const int32_t o_lane = o_batch + incl - cnt;
-		const bool fit = incl <= OW && incl_s <= MAXSEQ;
+		const bool fit = incl <= LZ4ADA_OW_CUT && incl_s <= LZ4ADA_SEQ_CUT;
 		const int32_t m = __popcll(__ballot(fit));  // lanes [0, m) form an LDS batch
 		ISTAMP(D_WALK1);
 
@@ -2579,6 +2586,11 @@ int idx_fused_mode(uint32_t nblocks)
 	if (hipGetDevice(&dev) == hipSuccess)
 		(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
 	return nblocks <= uint32_t(4 * cus) ? 4 : 3;
+}
+
+const char* idx_fused_kernel_name(uint32_t nblocks)
+{
+	return idx_fused_mode(nblocks) == 4 ? "k_decode_idx2" : "k_decode_idx";
 }
 
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,

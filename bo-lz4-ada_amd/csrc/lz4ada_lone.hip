@@ -407,14 +407,19 @@ __global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ 
 		// where its entry meets the stored one (the rest of that run was
 		// already right); the next pass confirms, or finds the next run
 		// (profiles/r04o_chain_walk.txt: a linked 256 KiB frame at 512-byte
-		// windows 24 -> 11 us against walking every remaining window).
+		// windows 24 -> 11 us against walking every remaining window).  The
+		// short walks are capped: from pass 2 + SHORT_WALKS on the
+		// lane walks every remaining window, so inputs with many short wrong
+		// runs cost at most a few passes more than the walk-to-the-end did.
+		constexpr uint32_t SHORT_WALKS = 3;
 		if (it >= 2) {
 			if (tid == 0) {
+				const bool to_end = it >= 2 + SHORT_WALKS;
 				for (int32_t w = first_ch; w < nwin; ++w) {
 					const uint32_t e = E[w];
 					const uint32_t lim = uint32_t(min((w + 1) * LW, n));
 					const uint32_t x = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
-					if (w > first_ch && E[w + 1] == x)
+					if (!to_end && w > first_ch && E[w + 1] == x)
 						break;
 					E[w + 1] = x;
 				}

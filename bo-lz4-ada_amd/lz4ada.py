@@ -212,6 +212,7 @@ _sig = {
     "lz4ada_decode_frame_partial": ([_vp, _i64, _P(_vp), _pi64, _pi64], ctypes.c_int),
     "lz4ada_buffer_free": ([_vp], None),
     "lz4ada_last_path": ([], ctypes.c_int),
+    "lz4ada_bulk_decoder_kernel": ([ctypes.c_int64], ctypes.c_char_p),
     "lz4ada_release_device_cache": ([], None),
     "lz4ada_decode_linked_device": ([_vp, ctypes.c_uint64, _vp, _i64, _i64, _vp, _i64, _pi64, _vp],
                                     ctypes.c_int),
@@ -512,6 +513,11 @@ def multi_device_allocs(device: int) -> int:
 def rccl_version() -> int:
     """ncclGetVersion of the RCCL this process bound (22606 = 2.26.6)."""
     return int(_lib.lz4ada_rccl_version())
+
+
+def bulk_decoder_kernel(nblocks: int) -> str:
+    """The kernel the product bulk call launches for `nblocks` blocks."""
+    return _lib.lz4ada_bulk_decoder_kernel(nblocks).decode()
 
 
 def last_path() -> int:

@@ -256,6 +256,11 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
 int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,
                                  lz4ada_block_status *d_status, int variant, void *stream);
+/* The name of the kernel the fused bulk decode (LZ4ADA_DECODE_IDX, the
+ * product call lz4ada_decode_blocks_device) launches for nblocks blocks --
+ * it depends on how the block count fills the chip (for benches and
+ * profiles; a static string). */
+const char *lz4ada_bulk_decoder_kernel(int64_t nblocks);
 
 /* One block (payload d_blk, n bytes, no history) decoded by the whole GPU
  * (lz4ada_lone.hip: every byte position parsed, the sequence chain found by

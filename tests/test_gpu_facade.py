@@ -302,6 +302,39 @@ def test_facade_linked_d1_block_on_gpu(lit_len, off):
         assert exact == 0, exact
 
 
+def d1_frame_mid(mid_len, lit_len, off, tail=b"vwxyz"):
+    """d1_frame with a small literal-only linked block of mid_len bytes
+    between the 64 KiB block and the D1 block, so the D1 block starts at
+    Output_Pos = mid_len of its round (n1 > 0) instead of at 0."""
+    import struct
+    comp0, raw0 = lz4ada.gen_block(1, 1234, 65536)
+    mid = bytes(97 + i % 26 for i in range(mid_len))
+    comp_mid = bytes([(min(mid_len, 15) << 4)]) + (bytes([mid_len - 15]) if mid_len >= 15 else b"") + mid
+    lits = bytes(range(65, 65 + lit_len))
+    tok = (min(lit_len, 15) << 4) | 6
+    ext = bytes([lit_len - 15]) if lit_len >= 15 else b""
+    comp1 = bytes([tok]) + ext + lits + struct.pack("<H", off) + bytes([len(tail) << 4]) + tail
+    frame, _ = lz4frame.build_frame([(comp0, raw0, False), (comp_mid, mid, False), (comp1, b"", False)],
+                                    64 * KiB, indep=False)
+    return frame
+
+
+@pytest.mark.parametrize("mid_len,lit_len,off", [(1, 20, 65533), (3, 1, 65535), (9, 7, 65530),
+                                                 (12, 13, 65534), (40, 5, 65535), (200, 16, 65532)])
+def test_facade_linked_d1_block_after_small_block(mid_len, lit_len, off):
+    """the D1 shape in a LATER block of its round (a small linked
+    block between the 64 KiB block and the D1 block; k_lone_words uses the
+    block's position in the round, n1, in the D1 condition and in the
+    cross-round decline).  Call by call equal to the oracle at both feeds;
+    the 64 KiB and the small block never take the exact path, the D1 block
+    at most once per feed."""
+    frame = d1_frame_mid(mid_len, lit_len, off)
+    for feed in (0, 4096):
+        ours, exact = trace_ours_ctx(frame, feed)
+        assert ours == trace_oracle(frame, feed)
+        assert exact <= 1, exact
+
+
 def test_facade_linked_d1_without_literals_goes_exact():
     """Quirk D1 after a match rather than literals (the last write's
     overshoot comes from the Buffer): not emulated -- the exact path, the
