@@ -76,6 +76,8 @@ def parse_args(argv=None):
                     help="skip the configs[1] row (1 GiB frame, 64 KiB blocks)")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the c3_one_gpu row (configs[3]'s 32 GiB frame on one GPU)")
+    ap.add_argument("--no-facade", action="store_true",
+                    help="skip the facade row (Update at 4 KiB reads from C, SURVEY §8f item 1)")
     ap.add_argument("--launch-check", action="store_true",
                     help="test hook: start the ranks, check the process group (gloo, no GPU), "
                          "print one JSON line")
@@ -556,6 +558,68 @@ def bench_64k(M, dev, sh, stream, kind="mixed", nblocks=16384, bmax=64 * 1024, u
             "compressed_bytes": comp, "decoded_bytes": raw}
 
 
+def bench_facade(feed=4096, reps=5):
+    """the streaming facade (Init_With_Header + Update)
+    driven from C the way tool_unlz4ada drives the library -- 4 KiB reads
+    (tool_unlz4ada/unlz4ada.adb:16, 84-103), a context per frame -- on three
+    frames with block and content checksums: 64 KiB independent blocks (the
+    LZ4F default block size), 256 KiB linked blocks, 4 MiB independent
+    blocks.  Each is timed next to the oracle's 1-core loop over the same
+    frame (the reference's CPU path, 4 KiB reads).  Host-resident input and
+    output: this is the facade's latency path, not the bulk roofline."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    import lz4ada
+    import lz4frame
+    exe = os.path.join(ROOT, "bo-lz4-ada_amd", "facade_bench")
+    L = O.lib()
+    cases = [("indep_64k", 64 << 10, 64, True), ("linked_256k", 256 << 10, 32, False),
+             ("indep_4m", 4 << 20, 8, True)]
+    rows = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, bmax, nb, indep in cases:
+            if indep:
+                blocks = [(*lz4ada.gen_block(lz4ada.GEN_KINDS["mixed"], SEED0 + i, bmax), False)
+                          for i in range(nb)]
+            else:  # offsets below 65529: no block meets quirk D1 (DESIGN §6)
+                blocks = [(c, r, False) for c, r in
+                          lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS["mixed_nod1"], SEED0, bmax, nb)]
+            frame, _ = lz4frame.build_frame(blocks, bmax, indep=indep, block_cksum=True,
+                                            content_cksum=True)
+            st, expect, msg = O.unlz4ada(frame, out_cap=len(frame) * 4 + (8 << 20))
+            assert st == O.OK, msg
+            path = os.path.join(td, name + ".lz4")
+            with open(path, "wb") as fh:
+                fh.write(frame)
+            with open(path + ".out", "wb") as fh:
+                fh.write(expect)
+            r = subprocess.run([exe, path, str(feed), str(reps)], capture_output=True, text=True,
+                               timeout=300)
+            assert r.returncode == 0, f"facade_bench {name}: {r.stderr[-500:]}"
+            row = json.loads(r.stdout.strip().splitlines()[-1])
+            # the oracle's loop over the same frame, best of three
+            out = ctypes.create_string_buffer(len(expect) + (1 << 20))
+            n = ctypes.c_int64()
+            err = ctypes.create_string_buffer(512)
+            best = None
+            for _ in range(3):
+                t0 = time.perf_counter()
+                st = L.oracle_unlz4ada(frame, len(frame), out, len(expect) + (1 << 20),
+                                       ctypes.byref(n), err, 512)
+                dt = time.perf_counter() - t0
+                assert st == O.OK and n.value == len(expect)
+                best = dt if best is None else min(best, dt)
+            row["oracle_1core_mib_s"] = round(len(expect) / best / MiB, 1)
+            row["frame"] = (f"{nb} x {bmax >> 10} KiB {'independent' if indep else 'linked'} mixed "
+                            f"blocks, block + content checksum, {len(expect) / MiB:.0f} MiB decoded")
+            rows[name] = row
+    rows["note"] = (f"bo-lz4-ada_amd/facade_bench: {feed}-byte Update calls from C, median of {reps} "
+                    "frames, a context per frame, output checked; oracle_1core_mib_s: the oracle's "
+                    "unlz4ada loop over the same frame (1 core)")
+    return rows
+
+
 # ----------------------------------------------------------------------- main
 
 def launch_check(args):
@@ -808,6 +872,12 @@ def main():
     if extra and not args.no_64k:
         log("[bench] configs[1] 64 KiB row ...")
         result["c2_64k"] = bench_64k(M, dev, sh, stream)
+
+    # ---- the streaming facade at tool_unlz4ada's 4 KiB reads
+    if extra and not args.no_facade:
+        log("[bench] facade (4 KiB reads from C) ...")
+        torch.cuda.empty_cache()
+        result["facade"] = bench_facade()
 
     if extra and not args.no_cpu_baseline:
         log("[bench] CPU baseline (oracle) ...")

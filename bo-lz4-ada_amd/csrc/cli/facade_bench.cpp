@@ -1,11 +1,11 @@
-// facade_c -- the streaming facade timed from C (tool_unlz4ada's loop,
-// unlz4ada.adb:84-103, over the C-ABI): Init_With_Header, then Update with
-// `feed`-byte reads until End_Of_Frame, the delivered bytes appended to an
-// output buffer and compared with the expected output once.  No Python in
-// the loop, so the per-call cost is the library's own.
-//   g++ -O2 -std=c++17 -Iinclude -o tools/facade_c tools/facade_c.cpp
-//       -Lbo-lz4-ada_amd -llz4ada_hip -Wl,-rpath,$PWD/bo-lz4-ada_amd
-//   tools/facade_c frame.lz4 4096 5     (frame.lz4.out: the expected bytes)
+// facade_bench -- the streaming facade timed from C (tool_unlz4ada's loop,
+// tool_unlz4ada/unlz4ada.adb:16, 84-103, over the C-ABI): Init_With_Header,
+// then Update with `feed`-byte reads until End_Of_Frame, the delivered bytes
+// appended to an output buffer and compared with the expected output once.
+// No Python in the loop, so the per-call cost is the library's own.  Built
+// by csrc/Makefile as bo-lz4-ada_amd/facade_bench; bench.py's `facade` key
+// runs it (the last line of its output is one JSON object).
+//   facade_bench frame.lz4 4096 5     (frame.lz4.out: the expected bytes)
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -115,5 +115,9 @@ int main(int argc, char** argv)
 		return 1;
 	printf("facade_c %s feed=%lld: %d frames through one context %.2f ms per frame  %.1f MiB/s, "
 	       "%lld exact blocks\n", argv[1], (long long)feed, K, t * 1e3 / K, mib * K / t, (long long)g_exact);
+	printf("{\"mib_s\": %.1f, \"mib_s_best\": %.1f, \"ms_per_frame\": %.3f, \"reps\": %d, "
+	       "\"mib_s_one_context\": %.1f, \"exact_blocks\": %lld}\n",
+	       mib / ts[ts.size() / 2], mib / ts[0], ts[ts.size() / 2] * 1e3, reps, mib * K / t,
+	       (long long)g_exact);
 	return 0;
 }

@@ -116,6 +116,22 @@ __device__ unsigned long long g_idx_stamps[IDX_NST];
 #define ISTAMP_FLUSH()
 #endif
 
+// Diagnostic build only (-DLZ4ADA_IDX_GATHERS): the 16-byte HBM loads of
+// k_decode_idx's HBM-sourced matches: loads, 128-byte line touches (a load
+// crossing a line boundary touches two; no de-duplication), batches -- to
+// price the gather share of FETCH_SIZE.
+#ifdef LZ4ADA_IDX_GATHERS
+__device__ unsigned long long g_idx_gathers[4];  // loads, line touches, batches, input stagings
+#define GCOUNT(i, v)                                                         \
+	do {                                                                     \
+		const uint64_t _v = uint64_t(v);                                     \
+		if (lane_id() == 0 && _v)                                            \
+			atomicAdd(&g_idx_gathers[i], (unsigned long long)_v);            \
+	} while (0)
+#else
+#define GCOUNT(i, v)
+#endif
+
 // ---------------------------------------------------------------- byte access
 // Block-relative byte p comes from LDS when [p, p+8) lies in the staged
 // window [lo, hi), else from global memory (guarded by the frame end).
@@ -1561,8 +1577,11 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
 #endif
 					nc[r] = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
+					GCOUNT(0, __popcll(__ballot(g)));
+					GCOUNT(1, __popcll(__ballot(g)) + __popcll(__ballot(g && ((src & 127) > 112))));
 				}
 			}
+			GCOUNT(2, 1);
 			static_assert(RMAX == 2, "HBM piece dealing pairs two rounds");
 			if (__any(nc[0] > 0 || nc[1] > 0)) {
 				const int32_t inc0 = wave_incl_scan(nc[0]);
@@ -1584,6 +1603,9 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				const int32_t od = o_batch + int32_t(dd & 0xffffu);
 				const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
 				const int32_t k = GC + lane - int32_t(dd >> 48);
+				GCOUNT(0, __popcll(__ballot(lane < tot)));
+				GCOUNT(1, __popcll(__ballot(lane < tot)) +
+				              __popcll(__ballot(lane < tot && ((od - ooff + 16 * k) & 127) > 112)));
 				if (lane < tot) {
 					rpd = od + 16 * k;
 					rpn = min(16, oml - 16 * k);
@@ -2515,841 +2537,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
-// ============================================================ pipelined pair
-// k_decode_pp (round 5): two waves per block that pipeline consecutive
-// batches instead of splitting each one (k_decode_idx2).  Every wave of the
-// one-wave kernel is latency-bound (issue 0.47, wait 0.46: DESIGN §4) and
-// the bench's 2048 blocks put only two of them on a SIMD; a block's serial
-// chain cannot be cut into independent output ranges (tools/taint_sim.cpp),
-// and two waves sharing one batch shorten it by 6-7% only (the batch's
-// latency is its LDS round trips and barriers).  Here wave w takes the
-// batches j = w, w + 2, ...: batch j's staging, cut, parse, HBM-sourced
-// match loads, literals and HBM-sourced stores run while the other wave is
-// still inside batch j - 1; only the ring-sourced matches (which may read
-// batch j - 1's output) wait for batch j - 1's to be stored (an LDS token),
-// and the flush follows.  Both waves compute every batch cut from the
-// staged pass-1 records (each its own batch and the next), so they agree on
-// the batch sequence, on who stages which input chunk and on the HBM
-// threshold without any barrier inside the batch loop; spin waits on LDS
-// counters (each also watching the abort flag) carry the hand-offs.
-//
-// Pass 1 of the block runs first: wave 0 walks the index (index_block's
-// rules) while wave 1 runs the block's XXH32 chain (B.Checksum,
-// lz4ada.adb:698-707) over the same staged chunks -- so no checksum kernel
-// runs beside this one and its VGPRs are free for the second decode wave
-// (four waves per SIMD at 2048 blocks, 128 VGPRs each).
-//
-// Ring discipline (8 KiB output window, batches of <= OWP bytes): during
-// batch j's ring-sourced matches, batch j + 1 (the other wave) may write its
-// literals and HBM-sourced bytes, so the window keeps at least
-// [o_j - RFLOOR, o_j + OWP) intact, RFLOOR = ORING - 2 OWP.  A match reads
-// HBM for the source bytes below glo_j = align16(o_{j-1}) -- written by the
-// flushes of batches <= j - 2, whose completion each wave publishes
-// (done[w]) after its own vmcnt wait -- and the ring for the rest (a match
-// straddling glo is split in two); glo_j > o_j - OWP - 16 > o_j - RFLOOR.
-// (Exactly: the split point is glo_j rounded down to a 128-byte line and a
-// match's HBM part ends in whole 16-byte pieces below it -- see OWP.)
-
-constexpr int OWP = 2672;                    // batch output limit (one round of 64 sequences)
-constexpr int32_t RFLOOR = ORING - 2 * OWP;  // ring bytes kept below a batch through its ring phase
-// HBM sources end below glo rounded down to a 128-byte line (a CU's L1 must
-// never cache a line holding bytes the other wave has not flushed yet: its
-// later readers would hit the stale copy), and a match's ring part starts
-// at most 15 bytes below that
-static_assert(OWP + 16 + 128 + 16 < RFLOOR, "the HBM threshold must lie inside the kept ring history");
-
-struct alignas(16) PpLds {
-	uint8_t ring[RING + 16];  // staged input: 4 chunks of 2 KiB (+ mirror), shared
-	uint8_t oring[ORING];     // output window, shared
-	uint64_t rrec[4 * 64];    // pass-1 records of the staged chunks
-	uint64_t ldesc[2][64];    // per wave: run / match descriptors of its dealt pieces
-	uint16_t cst[2][64];      // per wave: its batch's sequence starts
-	uint8_t own[2][64];       // per wave: piece owners
-	int32_t tok;              // last batch whose ring-sourced matches are stored
-	int32_t staged;           // input chunks staged so far
-	int32_t abort_;           // a wave declined the block
-	int32_t code;             // pass 1's verdict (wave 0 -> wave 1)
-	int32_t done[2];          // per wave: last own batch whose flush has completed
-	int32_t more;             // pass 1: another chunk follows (wave 0's walk or the hash needs it)
-	int32_t pad;
-};
-
-// Diagnostic build only (-DLZ4ADA_PP_STAMPS): per-phase wall cycles of
-// k_decode_pp summed over waves (s_memtime deltas; no memory drained, so a
-// phase's share includes the waits it really has).
-enum PpPhase { PS_PASS1, PS_WSTAGED, PS_STAGE, PS_CUT, PS_PRE, PS_HBMW, PS_LIT, PS_TOKW, PS_RING,
-	           PS_FLUSH, PS_OVER, PS_TAIL, PS_BATCHES, PS_WAVES, PP_NST };
-#ifdef LZ4ADA_PP_STAMPS
-__device__ unsigned long long g_pp_stamps[PP_NST];
-#define PPST_DECL uint64_t pst[PP_NST] = {}; uint64_t pst_t = __builtin_amdgcn_s_memtime()
-#define PPST(ph)                                                             \
-	do {                                                                     \
-		const uint64_t _n = __builtin_amdgcn_s_memtime();                    \
-		pst[ph] += _n - pst_t;                                               \
-		pst_t = _n;                                                          \
-	} while (0)
-#define PPCOUNT(ph, v) (pst[ph] += uint64_t(v))
-#define PPST_FLUSH()                                                         \
-	do {                                                                     \
-		if (lane_id() == 0)                                                  \
-			for (int _i = 0; _i < PP_NST; ++_i)                              \
-				atomicAdd(&g_pp_stamps[_i], (unsigned long long)pst[_i]);    \
-	} while (0)
-#else
-#define PPST_DECL
-#define PPST(ph)
-#define PPCOUNT(ph, v)
-#define PPST_FLUSH()
-#endif
-
-struct WP {
-	PpLds& L;
-	int32_t w;
-};
-__device__ __forceinline__ uint8_t (&oring_of(WP& V))[ORING] { return V.L.oring; }
-__device__ __forceinline__ const uint8_t (&oring_of(const WP& V))[ORING] { return V.L.oring; }
-__device__ __forceinline__ uint8_t* own_of(WP& V) { return V.L.own[V.w]; }
-__device__ __forceinline__ uint64_t* ldesc_of(WP& V) { return V.L.ldesc[V.w]; }
-
-__device__ __forceinline__ int32_t lds_peek(const int32_t* p)
-{
-	return __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile int32_t*>(p));
-}
-
-// Publish v at p after every LDS write of this wave so far (the other wave
-// reads those once it sees v): lgkmcnt(0) only -- the flush stores in
-// flight are not waited for.
-__device__ __forceinline__ void lds_publish(int32_t* p, int32_t v)
-{
-	asm volatile("" ::: "memory");
-	__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
-	*reinterpret_cast<volatile int32_t*>(p) = v;
-	asm volatile("" ::: "memory");
-}
-
-// Wait until *p >= want; false if the other wave aborted the block meanwhile
-// -- or after ~2^24 polls (~0.5 s): a hand-off that never comes declines the
-// block (DS_RETRY: the exact decoders redo it) instead of hanging the grid.
-__device__ __forceinline__ bool lds_wait_ge(PpLds& L, const int32_t* p, int32_t want)
-{
-	for (uint32_t it = 0; lds_peek(p) < want; ++it) {
-		if (lds_peek(&L.abort_))
-			return false;
-		if (it >= (1u << 24)) {
-			lds_publish(&L.abort_, 1);
-			return false;
-		}
-		__builtin_amdgcn_s_sleep(1);
-	}
-	asm volatile("" ::: "memory");
-	return true;
-}
-
-// One batch cut from the staged records (both waves compute every cut the
-// same way): sub-segments [k0, k0 + m) form the batch (<= 64 sequences,
-// <= OWP output bytes), `bytes` its output.  over: the first sub-segment
-// alone exceeds a limit -- the 64 sub-segments from k0 go straight to HBM.
-struct PpCut {
-	int32_t m, bytes;
-	bool over;
-};
-__device__ __forceinline__ PpCut pp_cut(const PpLds& L, int32_t k0, int32_t nsub)
-{
-	const int32_t k = k0 + int32_t(lane_id());
-	const uint64_t rec = k < nsub ? L.rrec[k & 255] : 0;
-	const int32_t cnt = int32_t(min(uint32_t(rec >> 32), 1u << 24));
-	const int32_t incl = wave_incl_scan(cnt);
-	const int32_t incl_s = wave_incl_scan(__popc(uint32_t(rec)));
-	PpCut c;
-	c.m = __popcll(__ballot(incl <= OWP && incl_s <= 64));
-	c.over = c.m == 0;
-	if (c.over) {
-		c.m = 64;
-		c.bytes = __shfl(incl, 63);
-	} else {
-		c.bytes = __shfl(incl, c.m - 1);
-	}
-	return c;
-}
-
-// ---- pass 1 with the block checksum beside it
-
-// XXH32 over up to 16 stripes from LDS (lane 4m + i loads word i of stripe
-// m and pre-multiplies it; ds_bpermute hands stripe m's four products to
-// every quad, so every quad runs the same four-accumulator chain: three
-// dependent VALU per stripe, ~17 cycles -- k_xxh32_rows' DPP quad hand-off
-// adds the DPP hazard to each step, ~55 cycles).
-__device__ __forceinline__ uint32_t pp_xxh16(uint32_t acc, uint32_t word, int32_t cnt)
-{
-	const uint32_t x = word * P2;
-	const int32_t q = int32_t(lane_id() & 3u);
-	uint32_t xs[16];
-#pragma unroll
-	for (int m = 0; m < 16; ++m)
-		xs[m] = __shfl(x, 4 * m + q);
-	if (cnt >= 16) {
-#pragma unroll
-		for (int m = 0; m < 16; ++m)
-			acc = rotl32(acc + xs[m], 13) * P1;
-	} else {
-#pragma unroll
-		for (int m = 0; m < 16; ++m)
-			if (m < cnt)
-				acc = rotl32(acc + xs[m], 13) * P1;
-	}
-	return acc;
-}
-
-// Pass 1 of block b by the two waves: both stage each 16 KiB chunk, wave 0
-// walks it (index_block's rules: lead-in, segment walks to a fixed point,
-// records to HBM), wave 1 advances the block's XXH32 over it.  Returns the
-// pass-1 verdict (DS_OK / DS_RETRY / DS_SPARSE) in both waves; the block
-// checksum goes to status[b].cksum.
-__device__ __forceinline__ int32_t index_block_pp(IdxLds& X, int32_t* shared4,
-                                                  const uint8_t* __restrict__ frame, uint64_t frame_len,
-                                                  const lz4ada_block_desc* __restrict__ desc, uint32_t b,
-                                                  uint8_t* __restrict__ tab_all,
-                                                  lz4ada_block_status* __restrict__ status)
-{
-	const int32_t tid = int32_t(threadIdx.x), w = tid >> 6, lane = tid & 63;
-	const lz4ada_block_desc d = desc[b];
-	const int32_t n = int32_t(d.in_len);
-	const bool stored = (d.flags & LZ4ADA_BLOCK_STORED) != 0;
-	const bool hash = (d.flags & LZ4ADA_BLOCK_HAS_CKSUM) != 0;
-	bool walk = !stored;
-	int32_t code = DS_OK;
-	if (walk && d.in_len >= RLE_MIN_IN && uint64_t(d.in_len) * RLE_RATIO < uint64_t(d.out_cap)) {
-		walk = false;
-		code = DS_SPARSE;
-	}
-	cg8* in = gptr(frame) + d.in_off;
-	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
-	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
-	uint64_t* tab = reinterpret_cast<uint64_t*>(tab_all) + (((d.in_off >> 8) + b) << 3);
-	Src S;
-	S.lds = X.buf;
-	S.mask = CHUNK - 1;
-	S.mis = mis;
-	S.in = in;
-	S.lim = lim;
-	constexpr int PF = CHUNK / 2048;  // 16-byte loads per thread per chunk
-	auto load16k = [&](uintptr_t a, u32x4 (&v)[PF]) {
-		if (a + CHUNK <= lim) {
-#pragma unroll
-			for (int r = 0; r < PF; ++r)
-				__builtin_memcpy(&v[r], reinterpret_cast<cg8*>(a + uintptr_t(2048 * r + 16 * tid)), 16);
-		} else {
-#pragma unroll
-			for (int r = 0; r < PF; ++r)
-				v[r] = gload16(a + uintptr_t(2048 * r + 16 * tid), lim);
-		}
-	};
-	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
-	u32x4 pf[PF];
-	const bool any = n > 0 && (walk || hash);
-	if (any)
-		load16k(abase, pf);
-
-	// wave 1: the XXH32 state (lane 4m + i carries accumulator i, every quad alike)
-	const uint32_t init[4] = { P1 + P2, P2, 0u, 0u - P1 };
-	uint32_t acc = init[lane & 3];
-	const int32_t nstripes = n >> 4;
-	uint32_t strad = 0;  // the stripe straddling the next chunk boundary (word lane & 3), from HBM
-
-	// wave 0: the walk state (index_block)
-	int32_t E = 0, lead = LEAD_IN0;
-	bool bad = false, sparse = false;
-	bool more = any;
-	for (int32_t C = 0; more; C += CHUNK) {
-#pragma unroll
-		for (int r = 0; r < PF; ++r)
-			*reinterpret_cast<u32x4*>(&X.buf[2048 * r + 16 * tid]) = pf[r];
-		if (tid == 0)
-			*reinterpret_cast<u32x4*>(&X.buf[CHUNK]) = pf[0];
-		__syncthreads();
-		const bool last = C + CHUNK >= n;
-		if (!last)
-			load16k(abase + uintptr_t(C + CHUNK), pf);
-		const int32_t lo = C - mis;  // payload offset of X.buf[0]
-		if (w == 1) {
-			if (hash) {
-				// the stripe straddling this chunk's start (loaded during the
-				// previous chunk), then the stripes inside the chunk
-				int32_t s = (max(lo, 0) + 15) >> 4;
-				if (C > 0 && (lo & 15) && (lo >> 4) < nstripes)
-					acc = rotl32(acc + strad * P2, 13) * P1;
-				const int32_t se = min((lo + CHUNK) >> 4, nstripes);
-				if (!last && ((lo + CHUNK) & 15) && se < nstripes) {
-					// next chunk's straddler: word (lane & 3) of stripe se
-					const uintptr_t g = reinterpret_cast<uintptr_t>(in) + uintptr_t(16 * se + 4 * (lane & 3));
-					strad = ld32u_cached(reinterpret_cast<cg8*>(g));
-				}
-				for (; s < se; s += 16) {
-					const int32_t o = min(16 * s - lo + 4 * lane, CHUNK - 4);  // lanes past se: any word
-					const uint32_t* wa = reinterpret_cast<const uint32_t*>(X.buf + (o & ~3));
-					const uint32_t word = __builtin_amdgcn_alignbyte(wa[1], wa[0], uint32_t(o & 3));
-					acc = pp_xxh16(acc, word, min(se - s, 16));
-				}
-			}
-		} else if (walk) {
-			S.lo = lo;
-			S.hi = lo + CHUNK;
-			const int32_t s = C + SEG * lane;
-			const int32_t seg_end = min(s + SEG, n);
-			int32_t ein = (lane == 0) ? E : s;
-			if (lane > 0 && s < n) {
-				int32_t p = max(s - lead, C);
-				while (p < s)
-					p = skip_seq(S, p);
-				ein = p;
-			}
-			uint32_t* ghi = reinterpret_cast<uint32_t*>(tab + (C >> 5) + NSUB * lane) + 1;
-			int32_t epos = INT32_MAX;
-			bool err = false;
-			int32_t nst = 0;
-			int32_t y = (s < n) ? walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, err,
-			                                   epos, 0, false, nst)
-			                    : ein;
-			for (int it = 0; it < 64; ++it) {
-				int32_t prev = __shfl_up(wave_incl_max(y), 1);
-				if (lane == 0)
-					prev = E;
-				const bool changed = prev != ein;
-				if (!__any(changed))
-					break;
-				if (changed) {
-					ein = prev;
-					if (s < n) {
-						y = walk_segment(S, ein, s, seg_end, n, X.rbm[lane], X.rcnt[lane], ghi, err, epos, y,
-						                 !err, nst);
-					} else {
-						y = ein;
-						err = false;
-					}
-				}
-			}
-			bad = __any(s < n && err);
-			wave_lds_fence();
-			int32_t starts = 0;
-#pragma unroll
-			for (int i = 0; i < NSUB; ++i) {
-				const int32_t r = 64 * i + lane, sg = r / NSUB, sb = r & (NSUB - 1);
-				if (C + SEG * sg < n) {
-					const uint32_t bmv = X.rbm[sg][sb], c16 = X.rcnt[sg][sb];
-					starts += __popc(bmv);
-					if (c16 != 0xFFFFu)
-						tab[(C >> 5) + r] = uint64_t(bmv) | (uint64_t(c16) << 32);
-					else
-						*reinterpret_cast<uint32_t*>(tab + (C >> 5) + r) = bmv;
-				}
-			}
-			E = __shfl(wave_incl_max(y), 63);
-			lead = lead_in_bytes(__shfl(wave_incl_scan(starts), 63));
-			if (C == 0 && n >= 4 * CHUNK && !bad) {
-				int32_t used = 0;
-				if (s < n)
-					for (int k = 0; k < NSUB; ++k)
-						used += X.rbm[lane][k] ? 1 : 0;
-				if (__shfl(wave_incl_scan(used), 63) < CHUNK / SUB / 4)
-					bad = sparse = true;
-			}
-			if (bad) {
-				walk = false;
-				code = sparse ? DS_SPARSE : DS_RETRY;
-			}
-			if (last && walk && E != n) {
-				walk = false;
-				code = DS_RETRY;
-			}
-		}
-		// the next chunk is staged while the walk or the hash still needs one
-		// (wave 0 decides; the flag alternates between two words so the next
-		// chunk's write cannot race this chunk's read)
-		const int32_t fi = 2 + ((C / CHUNK) & 1);
-		if (w == 0 && lane == 0)
-			shared4[fi] = (!last && (walk || hash)) ? 1 : 0;
-		__syncthreads();  // also: every read of this chunk's staging is done
-		more = shared4[fi] != 0;
-	}
-	if (w == 1 && hash) {
-		// every quad carries the chain: accumulator i in lane i
-		const uint32_t v0 = __shfl(acc, 0), v1 = __shfl(acc, 1), v2 = __shfl(acc, 2), v3 = __shfl(acc, 3);
-		if (lane == 0) {
-			uint32_t h = uint32_t(n);
-			h += n >= 16 ? rotl32(v0, 1) + rotl32(v1, 7) + rotl32(v2, 12) + rotl32(v3, 18) : P5;
-			cg8* t = in + 16 * nstripes;
-			const int32_t tl = n - 16 * nstripes;
-			int32_t q = 0;
-			for (; q + 4 <= tl; q += 4) {
-				const uint32_t wv = uint32_t(t[q]) | (uint32_t(t[q + 1]) << 8) | (uint32_t(t[q + 2]) << 16) |
-				                    (uint32_t(t[q + 3]) << 24);
-				h = rotl32(h + wv * P3, 17) * P4;
-			}
-			for (; q < tl; ++q)
-				h = rotl32(h + uint32_t(t[q]) * P5, 11) * P1;
-			h = (h ^ (h >> 15)) * P2;
-			h = (h ^ (h >> 13)) * P3;
-			h ^= h >> 16;
-			status[b].cksum = h;
-		}
-	}
-	if (w == 0 && lane == 0) {
-		status[b].code = code;
-		shared4[1] = code;
-	}
-	__syncthreads();
-	return shared4[1];
-}
-
-// ---- pass 2: the two waves pipeline consecutive batches
-
-// 2 KiB input chunk c and its 64 records, into registers (one wave)
-__device__ __forceinline__ void pp_load_chunk(uintptr_t abase, int32_t c, uintptr_t lim, const uint64_t* tab,
-                                              int32_t nsub, u32x4& v0, u32x4& v1, uint64_t& r)
-{
-	load_chunk2(abase, c, lim, v0, v1);
-	const int32_t k = 64 * c + int32_t(lane_id());
-	r = k < nsub ? __builtin_nontemporal_load(tab + k) : 0;
-}
-
-__device__ __forceinline__ void pp_stage_chunk(PpLds& L, int32_t c, const u32x4& v0, const u32x4& v1,
-                                               uint64_t r)
-{
-	const uint32_t lane = lane_id();
-	const uint32_t a = uint32_t(c * BATCH) & (RING - 1);
-	*reinterpret_cast<u32x4*>(&L.ring[a + 16 * lane]) = v0;
-	*reinterpret_cast<u32x4*>(&L.ring[a + 1024 + 16 * lane]) = v1;
-	if (a == 0 && lane == 0)
-		*reinterpret_cast<u32x4*>(&L.ring[RING]) = v0;
-	L.rrec[64 * (c & 3) + lane] = r;
-}
-
-// Pass 2 of block b (independent blocks; pass 1's verdict DS_OK).  Returns
-// the block's output length, or -1 when it declines (status DS_RETRY).
-__device__ __forceinline__ int32_t decode_block_pp(PpLds& L, const uint8_t* __restrict__ frame,
-                                                   uint64_t frame_len,
-                                                   const lz4ada_block_desc* __restrict__ desc, uint32_t b,
-                                                   const uint8_t* __restrict__ tab_all, uint8_t* __restrict__ out)
-{
-	const int32_t tid = int32_t(threadIdx.x), w = tid >> 6, lane = tid & 63;
-	WP V{ L, w };
-	const lz4ada_block_desc d = desc[b];
-	cg8* in = gptr(frame) + d.in_off;
-	g8* ob = gptr(out) + d.out_off;
-	const int32_t n = int32_t(d.in_len);
-	const int32_t cap = int32_t(d.out_cap);
-	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
-	const uintptr_t olim = reinterpret_cast<uintptr_t>(ob) + uintptr_t(cap);
-	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
-	const uint64_t* tab = reinterpret_cast<const uint64_t*>(tab_all) + (((d.in_off >> 8) + b) << 3);
-	const int32_t nsub = (n + SUB - 1) / SUB;
-	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
-
-	Src S;
-	S.lds = L.ring;
-	S.mask = RING - 1;
-	S.mis = mis;
-	S.in = in;
-	S.lim = lim;
-
-	// The cut cursor: the next batch to cut is j, at sub-segment k0 and
-	// output byte o; hi = input chunks staged once the batches cut so far
-	// have staged theirs (the owner of batch j stages [hi_before, cf_j + 3)).
-	// o_prev / over_prev: batch j - 1's output start and whether it went
-	// straight to HBM.  Each wave cuts its own batch and the next one (the
-	// other wave's), so both see the same sequence.
-	int32_t j = 0, k0 = 0, o = 0, hi = 0, o_prev = 0;
-	bool over_prev = false;
-	auto advance = [&](PpCut& c) {
-		c = pp_cut(L, k0, nsub);
-		o_prev = o;
-		over_prev = c.over;
-		o += c.bytes;
-		k0 += c.m;
-		++j;
-	};
-	auto chunk_of = [&](int32_t k) { return (k * SUB + mis) / BATCH; };
-	// this wave's prefetched chunk (its next batch stages it)
-	u32x4 pf0 = u32x4{ 0u, 0u, 0u, 0u }, pf1 = pf0;
-	uint64_t pr = 0;
-	int32_t pfc = -1;
-	bool bad = false;
-	PPST_DECL;
-	if (w == 1 && k0 < nsub) {  // batch 0 is wave 0's: cut it once staged
-		hi = chunk_of(0) + 3;
-		PpCut c0;
-		if (lds_wait_ge(L, &L.staged, hi))
-			advance(c0);
-		else
-			bad = true;
-	}
-
-	while (!bad && k0 < nsub) {
-		// ---- batch j is this wave's
-		const int32_t jb = j, ob0 = o, kb = k0;
-		const bool prev_over = over_prev;
-		// HBM holds, complete, every byte below glo: batches <= j - 2, or all
-		// of batch j - 1 when it went straight to HBM
-		const int32_t glo = jb == 0 ? 0 : ((prev_over ? ob0 : o_prev) & ~15);
-		const int32_t cf = chunk_of(kb);
-		const int32_t hi_before = hi;
-		hi = max(hi, cf + 3);
-		// staging: chunks [hi_before, hi) from this wave's prefetch when it
-		// holds the chunk, else loaded now; the chunks before are the other
-		// wave's (wait for them)
-		PPST(PS_TAIL);
-		PPCOUNT(PS_BATCHES, 1);
-		if (!lds_wait_ge(L, &L.staged, hi_before)) {
-			bad = true;
-			break;
-		}
-		PPST(PS_WSTAGED);
-		for (int32_t c = hi_before; c < hi; ++c) {
-			if (c != pfc) {
-				pp_load_chunk(abase, c, lim, tab, nsub, pf0, pf1, pr);
-				__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a rare path's loads settle here
-			}
-			pp_stage_chunk(L, c, pf0, pf1, pr);
-			pfc = -1;
-		}
-		if (hi > hi_before)
-			lds_publish(&L.staged, hi);
-		S.lo = cf * BATCH - mis;
-		S.hi = hi * BATCH - mis;
-		PPST(PS_STAGE);
-		// this batch's cut, then the next one's (the other wave's: its
-		// records are staged already, chunks <= cf + 2), which places this
-		// wave's next batch: prefetch the chunk that batch will stage
-		PpCut cb;
-		advance(cb);
-		const int32_t oe = o;  // this batch's output end
-		bool next_over = false;
-		int32_t npf = 0;       // vector loads issued after this wave's last flush
-		if (k0 < nsub) {
-			hi = max(hi, chunk_of(k0) + 3);
-			PpCut cn;
-			advance(cn);
-			next_over = cn.over;
-			if (k0 < nsub && chunk_of(k0) + 3 > hi) {
-				pfc = hi;
-				pp_load_chunk(abase, pfc, lim, tab, nsub, pf0, pf1, pr);
-				npf = 3;
-			}
-		}
-		PPST(PS_CUT);
-		if (oe > cap) {
-			bad = true;
-			lds_publish(&L.abort_, 1);
-			break;
-		}
-		if (cb.over) {
-			// ---- a sub-segment alone exceeds the batch limits: the 64
-			// sub-segments go straight to HBM (batch_global), alone -- after
-			// every earlier batch's bytes are final in HBM and in the window
-			if (!lds_wait_ge(L, &L.tok, jb - 1) || !lds_wait_ge(L, &L.done[w ^ 1], jb - 1)) {
-				bad = true;
-				break;
-			}
-			vm_wait();
-			const int32_t k = kb + lane;
-			const int32_t sub_s = k * SUB;
-			const int32_t sub_end = min(sub_s + SUB, n);
-			const uint64_t rec = (k < nsub) ? L.rrec[k & 255] : 0;
-			const uint32_t bm = uint32_t(rec);
-			const int32_t cnt = int32_t(min(uint32_t(rec >> 32), 1u << 24));
-			const int32_t p0 = bm ? sub_s + __builtin_ctz(bm) : n;
-			const int32_t incl = wave_incl_scan(cnt);
-			const int32_t a0 = ob0 & ~15;
-			if (lane == 0 && ob0 > a0)  // the window's unflushed tail
-				gstore_n(ob + a0, *reinterpret_cast<const u32x4*>(&L.oring[a0 & OMASK]), ob0 - a0);
-			vm_wait();
-			const bool ok = !__any(!batch_global(S, ob, olim, p0, sub_end, n, ob0 + incl - cnt, ob0, 0));
-			vm_wait();
-			if (!ok) {
-				bad = true;
-				lds_publish(&L.abort_, 1);
-				break;
-			}
-			// the window's history again, from HBM (nontemporal: past the L1,
-			// which may hold lines of this batch from before their stores)
-			const int32_t x0 = max(oe - ORING + 16, 0) & ~15;
-			for (int32_t x = x0 + 16 * lane; x < oe + 15; x += 64 * 16)
-				*reinterpret_cast<u32x4*>(&L.oring[uint32_t(x) & OMASK]) =
-				    x + 16 <= cap ? __builtin_nontemporal_load(reinterpret_cast<const GLOBAL u32x4*>(ob + x))
-				                  : gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(intptr_t(x)), olim);
-			__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-			lds_publish(&L.done[w], jb);
-			lds_publish(&L.tok, jb);
-			PPST(PS_OVER);
-			continue;
-		}
-		if (prev_over && !lds_wait_ge(L, &L.tok, jb - 1)) {
-			// the batch before went straight to HBM: its window reload lands
-			// before this batch writes the window
-			bad = true;
-			break;
-		}
-
-		// ---- the batch's sequence starts, in output order
-		const int32_t base = kb * SUB;
-		int32_t N;
-		{
-			const int32_t k = kb + lane;
-			const int32_t sub_s = k * SUB;
-			const uint64_t rec = (k < nsub) ? L.rrec[k & 255] : 0;
-			uint32_t bm = uint32_t(rec);
-			const int32_t nseq = __popc(bm);
-			const int32_t incl_s = wave_incl_scan(nseq);
-			if (lane < cb.m) {
-				int32_t e = incl_s - nseq;
-				const uint16_t rel = uint16_t(sub_s - base);
-				for (; bm; bm &= bm - 1)
-					L.cst[w][e++] = uint16_t(rel + __builtin_ctz(bm));
-			}
-			N = __shfl(incl_s, cb.m - 1);
-		}
-		wave_lds_fence();
-
-		// ---- P: this batch's sequences (<= 64), placed by a prefix sum
-		int32_t rL = 0, rlit = 0, roff = 0, rml = 0;
-		if (lane < N) {
-			Seq q;
-			parse_fast(S, base + int32_t(L.cst[w][lane]), n, q);
-			rL = q.L;
-			rlit = q.lit;
-			roff = q.off;
-			rml = q.ml;
-		}
-		const int32_t len = rL + rml;
-		const int32_t inc0 = wave_incl_scan(len);
-		const int32_t rdst = ob0 + inc0 - len;
-		const int32_t mdst = rdst + rL;
-		// a reference before the block start (D2): the block is declined
-		if (__any(rml > 0 && roff > mdst)) {
-			bad = true;
-			lds_publish(&L.abort_, 1);
-			break;
-		}
-		const int32_t src = mdst - roff;
-		// source bytes below glo come from HBM, the rest from the ring (a
-		// match straddling glo is split: hml bytes from HBM, then a ring
-		// match).  Every HBM load (16 bytes from a piece start) stays in the
-		// 128-byte lines wholly below glo: whole pieces only, unless the
-		// match's last piece fits too
-		const int32_t room = (glo & ~127) - src;
-		const int32_t hml = rml <= 0 ? 0 : (((rml + 15) & ~15) <= room ? rml : max(room & ~15, 0));
-		const int32_t lring = rml - hml;
-		const int32_t rdst2 = mdst + hml;
-
-		// ---- HBM-sourced bytes: this wave's flush of batch j - 2 first
-		// (npf: the prefetch loads issued after it may stay in flight), then
-		// the other wave's of batch j - 3; first piece in its own lane, the
-		// rest dealt
-		PPST(PS_PRE);
-		if (npf)
-			asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-		else
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		lds_publish(&L.done[w], max(jb - 2, -1));
-		u32x4 vg = u32x4{ 0u, 0u, 0u, 0u }, vr = vg;
-		int32_t rpd = 0, rpn = 0, rtot = 0;
-		if (__any(hml > 0)) {
-			if (!lds_wait_ge(L, &L.done[w ^ 1], jb - 3)) {
-				bad = true;
-				break;
-			}
-			if (hml > 0)
-				__builtin_memcpy(&vg, ob + src, 16);
-			const int32_t nc = hml > 0 ? max(((hml + 15) >> 4) - 1, 0) : 0;
-			if (__any(nc > 0)) {
-				const int32_t incc = wave_incl_scan(nc);
-				rtot = __shfl(incc, 63);
-				uint64_t* ldesc = ldesc_of(V);
-				ldesc[lane] = uint64_t(uint16_t(mdst - ob0)) | (uint64_t(uint16_t(roff)) << 16) |
-				              (uint64_t(uint16_t(hml)) << 32) | (uint64_t(uint16_t(incc - nc)) << 48);
-				const int32_t lo = min(chunk_owner(V, incc, nc, 0), 63);
-				const uint64_t dd = ldesc[lo];
-				const int32_t od = ob0 + int32_t(dd & 0xffffu);
-				const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
-				const int32_t kk = 1 + lane - int32_t(dd >> 48);
-				if (lane < rtot) {
-					rpd = od + 16 * kk;
-					rpn = min(16, oml - 16 * kk);
-					__builtin_memcpy(&vr, ob + (od - ooff) + 16 * kk, 16);
-				}
-				wave_lds_fence();
-			}
-		}
-
-		PPST(PS_HBMW);
-		// ---- L: literals, input ring -> output window (first piece in-lane)
-		if (rL > 0)
-			ostore(V, rdst, fetch16(S, rlit), min(16, rL));
-		{
-			const int32_t ncl = rL > 16 ? (rL - 1) >> 4 : 0;
-			if (__any(ncl > 0)) {
-				const int32_t incl2 = wave_incl_scan(ncl);
-				const int32_t tot = __shfl(incl2, 63);
-				uint64_t* ldesc = ldesc_of(V);
-				ldesc[lane] = uint64_t(uint16_t(rlit - base)) | (uint64_t(uint16_t(rdst - ob0)) << 16) |
-				              (uint64_t(uint16_t(rL)) << 32) | (uint64_t(uint16_t(incl2 - ncl)) << 48);
-				for (int32_t t0 = 0; t0 < tot; t0 += 64) {
-					const int32_t t = t0 + lane;
-					const int32_t lo = min(chunk_owner(V, incl2, ncl, t0), 63);
-					const uint64_t dd = ldesc[lo];
-					const int32_t lit = base + int32_t(dd & 0xffffu);
-					const int32_t dst = ob0 + int32_t((dd >> 16) & 0xffffu);
-					const int32_t Lx = int32_t((dd >> 32) & 0xffffu);
-					const int32_t kk = 1 + t - int32_t(dd >> 48);
-					if (t < tot)
-						ostore(V, dst + 16 * kk, fetch16(S, lit + 16 * kk), min(16, Lx - 16 * kk));
-				}
-			}
-		}
-		wave_lds_fence();
-
-		// ---- M, HBM-sourced stores (no order among them: sources in HBM)
-		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-		if (rpn > 0)
-			ostore(V, rpd, vr, rpn);
-		if (hml > 0)
-			ostore(V, mdst, vg, min(16, hml));
-		if (rtot > 64) {  // rare: more than 64 dealt pieces
-			const int32_t nc = hml > 0 ? max(((hml + 15) >> 4) - 1, 0) : 0;
-			const int32_t inc = wave_incl_scan(nc);
-			for (int32_t t0 = 64; t0 < rtot; t0 += 64) {
-				const int32_t t = t0 + lane;
-				const int32_t lo = piece_owner(inc, t);
-				const int32_t kk = 1 + t - (__shfl(inc, lo) - __shfl(nc, lo));
-				const int32_t osrc = __shfl(src, lo), odst = __shfl(mdst, lo);
-				const int32_t oml = __shfl(hml, lo);
-				if (t < rtot) {
-					u32x4 v;
-					__builtin_memcpy(&v, ob + osrc + 16 * kk, 16);
-					ostore(V, odst + 16 * kk, v, min(16, oml - 16 * kk));
-				}
-			}
-			__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-		}
-		wave_lds_fence();
-
-		PPST(PS_LIT);
-		// ---- ring-sourced matches, after batch j - 1's
-		if (!lds_wait_ge(L, &L.tok, jb - 1)) {
-			bad = true;
-			break;
-		}
-		PPST(PS_TOKW);
-		ring_round(V, rdst2, roff, lring, ob0, rL, ob0);
-		lds_publish(&L.tok, jb);
-		PPST(PS_RING);
-
-		// ---- flush whole 16-byte units of [ob0, oe) (the first may start
-		// before ob0: batch j - 1's bytes, final since its token)
-		{
-			const int32_t u0 = ob0 >> 4, u1 = oe >> 4;
-#pragma unroll
-			for (int i = 0; i < FLUSH_ST; ++i) {
-				const int32_t u = u0 + lane + 64 * i;
-				if (u < u1)
-					*reinterpret_cast<GLOBAL u32x4*>(ob + (u << 4)) =
-					    *reinterpret_cast<const u32x4*>(&L.oring[(u << 4) & OMASK]);
-			}
-		}
-		if (next_over) {
-			// the next batch goes straight to HBM once this flush is complete
-			vm_wait();
-			lds_publish(&L.done[w], jb);
-		}
-		PPST(PS_FLUSH);
-	}
-	PPST(PS_TAIL);
-	PPCOUNT(PS_WAVES, 1);
-	PPST_FLUSH();
-	// the last partial unit (after both waves' batches), by wave 0
-	__syncthreads();
-	bad = bad || lds_peek(&L.abort_) != 0;
-	if (!bad && tid == 0 && (o & 15))
-		gstore_n(ob + (o & ~15), *reinterpret_cast<const u32x4*>(&L.oring[(o & ~15) & OMASK]), o & 15);
-	return bad ? -1 : o;
-}
-
-// Independent blocks, both passes and the block checksums, two waves per
-// block pipelining batches.  Pinned to four waves per SIMD (128 VGPRs): LDS
-// allows 8 blocks = 16 waves per CU.
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_pp(
-        const uint8_t* __restrict__ frame, uint64_t frame_len, const lz4ada_block_desc* __restrict__ desc,
-        uint32_t nblocks, uint8_t* __restrict__ tab_all, uint8_t* __restrict__ out,
-        lz4ada_block_status* __restrict__ status)
-{
-	__shared__ union {
-		PpLds d;
-		IdxLds x;
-	} U;
-	__shared__ int32_t flags[4];
-	if (blockIdx.x >= nblocks)
-		return;
-	const uint32_t b = blockIdx.x;
-	const int32_t tid = int32_t(threadIdx.x), w = tid >> 6;
-#ifdef LZ4ADA_PP_STAMPS
-	const uint64_t t_p1 = __builtin_amdgcn_s_memtime();
-#endif
-	const int32_t code = index_block_pp(U.x, flags, frame, frame_len, desc, b, tab_all, status);
-#ifdef LZ4ADA_PP_STAMPS
-	if ((threadIdx.x & 63) == 0)
-		atomicAdd(&g_pp_stamps[PS_PASS1], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_p1));
-#endif
-	// the table this block's pass 1 wrote is read back by both waves
-	vm_wait();
-	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-	__syncthreads();
-	const lz4ada_block_desc d = desc[b];
-	if (code != DS_OK)
-		return;  // declined: its status says so (the block checksum is in place)
-	if (d.flags & LZ4ADA_BLOCK_STORED) {
-		const int32_t n = int32_t(d.in_len);
-		int32_t c = DS_OK;
-		if (n > int32_t(d.out_cap)) {
-			c = DS_OUT_OVERFLOW;
-		} else {  // each wave copies half (the checksum is done: nontemporal)
-			Src S0;
-			S0.in = gptr(frame) + d.in_off;
-			S0.lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
-			const int32_t mid = (n >> 1) & ~1023;
-			const int32_t c0 = w == 0 ? 0 : mid, c1 = w == 0 ? mid : n;
-			wave_literal<LZ4ADA_STORED_NT>(gptr(out) + d.out_off, c0, S0, c0, c1 - c0);
-		}
-		if (tid == 0) {
-			status[b].code = c;
-			status[b].aux = 0;
-			status[b].detail = 0;
-			status[b].err_out_pos = 0;
-			status[b].out_len = c == DS_OK ? uint32_t(n) : 0u;
-		}
-		return;
-	}
-	PpLds& L = U.d;
-	if (tid == 0) {
-		L.tok = -1;  // "batches <= -1 done"
-		L.staged = 0;
-		L.abort_ = 0;
-		L.done[0] = L.done[1] = -1;
-	}
-	__syncthreads();
-	const int32_t len = decode_block_pp(L, frame, frame_len, desc, b, tab_all, out);
-	if (tid == 0) {
-		if (len < 0) {
-			status[b].code = DS_RETRY;
-		} else {
-			status[b].code = DS_OK;
-			status[b].aux = 0;
-			status[b].detail = 0;
-			status[b].err_out_pos = 0;
-			status[b].out_len = uint32_t(len);
-		}
-	}
-}
-
 }  // namespace idx
 
 #ifdef LZ4ADA_IDX_STAMPS
@@ -3367,18 +2554,17 @@ extern "C" int lz4ada_idx_stamps(unsigned long long* out, int reset)
 }
 #endif
 
-#ifdef LZ4ADA_PP_STAMPS
-extern "C" int lz4ada_pp_stamps(unsigned long long* out, int reset)
+#ifdef LZ4ADA_IDX_GATHERS
+extern "C" int lz4ada_idx_gathers(unsigned long long* out, int reset)
 {
-	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(idx::g_pp_stamps), sizeof(unsigned long long) * idx::PP_NST) !=
-	    hipSuccess)
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(idx::g_idx_gathers), sizeof(unsigned long long) * 4) != hipSuccess)
 		return -1;
 	if (reset) {
-		unsigned long long z[idx::PP_NST] = {};
-		if (hipMemcpyToSymbol(HIP_SYMBOL(idx::g_pp_stamps), z, sizeof z) != hipSuccess)
+		unsigned long long z[4] = {};
+		if (hipMemcpyToSymbol(HIP_SYMBOL(idx::g_idx_gathers), z, sizeof z) != hipSuccess)
 			return -1;
 	}
-	return idx::PP_NST;
+	return 4;
 }
 #endif
 
@@ -3407,11 +2593,6 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 {
 	if (nblocks == 0)
 		return hipSuccess;
-	if (mode == 5) {  // both passes + block checksums, two waves pipelining batches (k_decode_pp)
-		hipLaunchKernelGGL(idx::k_decode_pp, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
-		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
-		return hipGetLastError();
-	}
 	if (mode == 4) {  // both passes, two waves per block (k_decode_idx2)
 		hipLaunchKernelGGL(idx::k_decode_idx2, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
 		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
@@ -3434,7 +2615,7 @@ int idx_fused_mode(uint32_t nblocks)
 {
 	static const int forced = [] {
 		const char* e = getenv("LZ4ADA_IDX_WAVES");
-		return e ? (e[0] == '1' ? 3 : (e[0] == '2' ? 4 : (e[0] == 'p' ? 5 : 0))) : 0;
+		return e ? (e[0] == '1' ? 3 : (e[0] == '2' ? 4 : 0)) : 0;
 	}();
 	if (forced)
 		return forced;
@@ -3446,8 +2627,7 @@ int idx_fused_mode(uint32_t nblocks)
 
 const char* idx_fused_kernel_name(uint32_t nblocks)
 {
-	const int m = idx_fused_mode(nblocks);
-	return m == 5 ? "k_decode_pp" : (m == 4 ? "k_decode_idx2" : "k_decode_idx");
+	return idx_fused_mode(nblocks) == 4 ? "k_decode_idx2" : "k_decode_idx";
 }
 
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
@@ -3460,8 +2640,8 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 	hipError_t err = hipMallocAsync(&tab, index_table_bytes(frame_len, nblocks), stream);
 	if (err != hipSuccess)
 		return err;
-	if (linked <= 0) {  // both passes in one launch (-1: one wave per block, -2: two, -3: pipelined pair)
-		const int mode = linked == -1 ? 3 : (linked == -2 ? 4 : (linked == -3 ? 5 : idx_fused_mode(nblocks)));
+	if (linked <= 0) {  // both passes in one launch (-1: one wave per block, -2: two)
+		const int mode = linked == -1 ? 3 : (linked == -2 ? 4 : idx_fused_mode(nblocks));
 		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
 		                            static_cast<const uint8_t*>(tab), d_out, d_status, mode, stream);
 	} else {

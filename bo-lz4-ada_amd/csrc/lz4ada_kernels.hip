@@ -1401,9 +1401,9 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 	}
 	if (variant == DEC_IDX_LINKED)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream, 1);
-	if (variant == DEC_IDX1_ALONE || variant == DEC_IDX2_ALONE || variant == DEC_PP_ALONE)
+	if (variant == DEC_IDX1_ALONE || variant == DEC_IDX2_ALONE)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream,
-		                         variant == DEC_IDX1_ALONE ? -1 : (variant == DEC_IDX2_ALONE ? -2 : -3));
+		                         variant == DEC_IDX1_ALONE ? -1 : -2);
 	if (variant == DEC_IDX || variant == DEC_IDX_ALONE || variant == DEC_IDX_SPARSE) {
 		const hipError_t err = launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out,
 		                                         d_status, stream);
@@ -1535,9 +1535,7 @@ hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
 		                                   idx_fused_mode(nblocks), stream)
 		           : launch_index(d_frame, frame_len, d_desc, nblocks, static_cast<uint8_t*>(tab),
 		                          d_status, stream);
-	// k_decode_pp computes the block checksums itself (its second wave, in
-	// pass 1): no checksum kernel beside it
-	if (err == hipSuccess && !(fuse && idx_fused_mode(nblocks) == 5))
+	if (err == hipSuccess)
 		err = launch_block_checksums(d_frame, d_desc, nblocks, d_status, side->s);
 	if (err == hipSuccess)
 		err = hipEventRecord(side->join, side->s);

@@ -276,7 +276,7 @@ def test_device_resident_blocks():
 
 # ------------------------------------------- bench-sized blocks (regression)
 
-@pytest.mark.parametrize("variant", ["pc", "idx", "idx1", "pp"])
+@pytest.mark.parametrize("variant", ["pc", "idx", "idx1"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "rle", "literal"])
 def test_bench_blocks_exact(kind, variant):
     """The bench's own unique 4 MiB blocks (seed 0x4C5A3441 + i) decode
@@ -295,10 +295,9 @@ def test_bench_blocks_exact(kind, variant):
     d_out = torch.zeros(nb * bmax, dtype=torch.uint8, device=dev)
     d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
     sh = torch.cuda.current_stream().cuda_stream
-    if variant != "pp":  # k_decode_pp computes the block checksums itself
-        lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), nb, d_st.data_ptr(), sh)
+    lz4ada.launch_block_checksums(d_frame.data_ptr(), d_desc.data_ptr(), nb, d_st.data_ptr(), sh)
     v = {"pc": lz4ada.DECODE_PC, "idx": lz4ada.DECODE_IDX,
-         "idx1": lz4ada.DECODE_IDX1_ALONE, "pp": lz4ada.DECODE_PP_ALONE}[variant]
+         "idx1": lz4ada.DECODE_IDX1_ALONE}[variant]
     lz4ada.launch_decode_variant(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
                                  d_out.data_ptr(), d_st.data_ptr(), v, sh)
     torch.cuda.synchronize()
@@ -307,7 +306,7 @@ def test_bench_blocks_exact(kind, variant):
     bad = []
     for i, (c, r) in enumerate(blocks):
         assert st[i].cksum == descs[i].cksum, (i, "block checksum")
-        if variant in ("idx1", "pp") and st[i].code == lz4ada.DS_SPARSE:
+        if variant == "idx1" and st[i].code == lz4ada.DS_SPARSE:
             continue  # the index decoder alone leaves these to k_decode_sparse
         got = out[i * bmax:i * bmax + len(r)]
         if st[i].code or st[i].out_len != len(r) or got != r:
@@ -361,7 +360,7 @@ def _run_variant_alone(frame, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["default", "idx1", "idx2", "pp"])
+@pytest.mark.parametrize("variant", ["default", "idx1", "idx2"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "rle", "chain"])
 @pytest.mark.parametrize("bmax", [64 << 10, 256 << 10, 4 << 20])
 def test_idx_decoder_alone(kind, bmax, variant):
@@ -375,14 +374,11 @@ def test_idx_decoder_alone(kind, bmax, variant):
     # ragged sizes: partial pass-1 chunks and batches, both waves' shares
     for j, n in enumerate((bmax - 1, bmax // 2 + 33, 16384 + 5, 4097, 200, 17, 1)):
         blocks.append(lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 900 + j, min(n, bmax)))
-    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, indep=True,
-                                      block_cksum=variant == "pp")
+    frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, indep=True)
     v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
-         "idx2": lz4ada.DECODE_IDX2_ALONE, "pp": lz4ada.DECODE_PP_ALONE}[variant]
+         "idx2": lz4ada.DECODE_IDX2_ALONE}[variant]
     descs, st, out = _run_variant_alone(frame, v)
     bad = []
-    if variant == "pp":  # the block checksums it computed in pass 1, every block
-        bad += [("cksum", i) for i in range(len(blocks)) if st[i].cksum != descs[i].cksum]
     for i, (c, r) in enumerate(blocks):
         if kind == "literal" and st[i].code == lz4ada.DS_SPARSE and len(c) >= 65536:
             continue
@@ -393,47 +389,6 @@ def test_idx_decoder_alone(kind, bmax, variant):
             j = next((k for k in range(min(len(r), len(got))) if got[k] != r[k]), -1)
             bad.append((i, st[i].code, st[i].out_len, len(r), j))
     assert not bad, bad
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("mis", [0, 1, 5, 15])
-def test_pp_block_checksums(mis):
-    """k_decode_pp's in-kernel block checksums (pass 1's second wave,
-    lz4ada.adb:698-707): every block of a frame with B.Checksum -- stored,
-    declined (sparse, RLE) and decoded ones, sizes around the 16-byte stripe
-    and the 16 KiB chunk, the payload shifted by `mis` bytes -- against the
-    declared checksum."""
-    import torch
-    blocks = []
-    sizes = [65536, 1, 0, 13, 15, 16, 17, 31, 33, 100, 4000, 16384, 16385, 32767, 65535]
-    for i, raw_len in enumerate(sizes):
-        if i % 5 == 4:
-            raw = random.Random(700 + i).randbytes(raw_len)
-            blocks.append((raw, raw, True))
-        else:
-            comp, raw = lz4ada.gen_block([1, 0, 3, 2][i % 4], 700 + i, raw_len)
-            blocks.append((comp, raw, False))
-    frame, raw = lz4frame.build_frame(blocks, 64 << 10, indep=True, block_cksum=True)
-    frame = bytes(mis) + frame  # every payload shifted off the 16-byte grid
-    info, descs = lz4ada.frame_index(frame, mis)
-    nb = info.nblocks
-    dev = torch.device("cuda:0")
-    d_frame = torch.frombuffer(bytearray(frame), dtype=torch.uint8).to(dev)
-    for i in range(nb):
-        descs[i].in_off += mis
-    d_desc = torch.frombuffer(bytearray(bytes(descs)[:nb * 32]), dtype=torch.uint8).to(dev)
-    d_out = torch.zeros(nb * info.block_max, dtype=torch.uint8, device=dev)
-    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
-    lz4ada.launch_decode_variant(d_frame.data_ptr(), len(frame), d_desc.data_ptr(), nb,
-                                 d_out.data_ptr(), d_st.data_ptr(), lz4ada.DECODE_PP_ALONE,
-                                 torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    st = (lz4ada.BlockStatus * nb).from_buffer_copy(d_st.cpu().numpy().tobytes())
-    out = d_out.cpu().numpy().tobytes()
-    for i in range(nb):
-        assert st[i].cksum == descs[i].cksum, (i, sizes[i])
-        if st[i].code == 0:
-            assert out[i * info.block_max:i * info.block_max + st[i].out_len] == blocks[i][1], i
 
 
 @pytest.mark.gpu
@@ -479,7 +434,7 @@ def oracle_blocks(frame, nblocks):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alone", ["default", "idx1", "idx2", "pp"])
+@pytest.mark.parametrize("alone", ["default", "idx1", "idx2"])
 @pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
 def test_idx_decoder_on_vectors(name, digests, alone):
     """Reference vectors' blocks through the idx decoder (+ retry): every block
@@ -488,12 +443,8 @@ def test_idx_decoder_on_vectors(name, digests, alone):
     frame = read_vector(name, "lz4")
     info, _ = lz4ada.frame_index(frame)
     v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
-         "idx2": lz4ada.DECODE_IDX2_ALONE, "pp": lz4ada.DECODE_PP_ALONE}[alone]
+         "idx2": lz4ada.DECODE_IDX2_ALONE}[alone]
     descs, st, out = _run_variant_alone(frame, v)
-    if alone == "pp":  # block checksums computed in pass 1, declined blocks included
-        for i in range(info.nblocks):
-            if descs[i].flags & lz4ada.BLOCK_HAS_CKSUM:
-                assert st[i].cksum == descs[i].cksum, (i, "block checksum")
     for i in range(info.nblocks):
         assert st[i].code in (0, lz4ada.DS_RETRY, lz4ada.DS_SPARSE), (i, st[i].code)
     ref = oracle_blocks(frame, info.nblocks)
