@@ -1,0 +1,222 @@
+// lz4ada_bulk_linked.cpp -- the linked-frame bulk path of the MI355X LZ4Ada
+// decompressor (BASELINE configs[4]): every block of a
+// linked frame (B.Indep = 0, the LZ4F default) decoded at once against
+// synthetic history, which lz4ada_linked.hip then resolves on the GPU by
+// pointer jumping; quirk D1 (lib/lz4ada.adb:811-817, 862-879)
+// and references before the frame start go to the exact path.
+#include "lz4ada_host_common.h"
+
+namespace lz4ada {
+
+// Linked frames (and independent ones whose blocks read earlier blocks,
+// D2): every block at once with synthetic history, resolved on the GPU
+// (lz4ada_linked.hip), batch by batch with the previous batch's last
+// 64 KiB carried as real history.  BULK_EXACT: the frame needs the exact
+// path (a block error or checksum mismatch, quirk D1, a reference before
+// the frame start, no device memory).
+BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block_max,
+                              const std::vector<lz4ada_block_desc>& descs, LinkedSink& sink,
+                              uint64_t& total, std::vector<uint32_t>& lens, int64_t& fail,
+                              hipStream_t stream, const LinkedHist* hist)
+{
+	lens.clear();
+	fail = -1;
+	// a batch holds 3 decode buffers (slots + 64 KiB regions) and one 4-byte
+	// word per output byte: ~7x its slot bytes
+	uint64_t budget = uint64_t(env_bytes("LZ4ADA_LINKED_BATCH_BYTES", int64_t(2) << 30));
+	// LZ4ADA_TRACE_LINKED=1: phase times (synchronised) to stderr
+	static const bool trace = getenv("LZ4ADA_TRACE_LINKED") != nullptr;
+	auto t0 = std::chrono::steady_clock::now();
+	auto phase = [&](const char* name) {
+		if (!trace)
+			return;
+		HIP_OK(hipStreamSynchronize(stream));
+		const auto t1 = std::chrono::steady_clock::now();
+		fprintf(stderr, "[linked] %-10s %8.3f ms\n", name,
+		        std::chrono::duration<double, std::milli>(t1 - t0).count());
+		t0 = t1;
+	};
+	DevBuf<uint8_t> d_tail[2];
+	d_tail[0].reserve(size_t(HISTORY_SIZE));
+	d_tail[1].reserve(size_t(HISTORY_SIZE));
+	HIP_OK(hipMemsetAsync(d_tail[0].p, 0, size_t(HISTORY_SIZE), stream));
+	int cur = 0;
+	// the reference's Output_Pos / Output_Pos_History (lz4ada.adb:678-690,
+	// 785-787), for quirk D1
+	int64_t opos = 0, oph = 0;
+	int64_t hist0 = 0;  // history bytes before the first block (mid-frame batch)
+	if (hist) {
+		hist0 = std::min<int64_t>(hist->n0 + hist->n1, HISTORY_SIZE);
+		if (hist->n1 > 0)
+			HIP_OK(hipMemcpyAsync(d_tail[0].p + HISTORY_SIZE - hist->n1, hist->h1, size_t(hist->n1),
+			                      hipMemcpyDeviceToDevice, stream));
+		if (hist->n0 > 0)
+			HIP_OK(hipMemcpyAsync(d_tail[0].p + HISTORY_SIZE - hist->n1 - hist->n0, hist->h0,
+			                      size_t(hist->n0), hipMemcpyDeviceToDevice, stream));
+		opos = hist->output_pos;
+		oph = hist->output_pos_history;
+	}
+	uint32_t lo = 0;
+	total = 0;
+	while (lo < descs.size()) {
+		const auto bt = batches_of(std::vector<lz4ada_block_desc>(descs.begin() + lo, descs.end()),
+		                           block_max, uint64_t(HISTORY_SIZE), budget);
+		const uint32_t hi = lo + bt[0].second;
+		uint32_t nb = hi - lo;
+		std::vector<lz4ada_block_desc> d(descs.begin() + lo, descs.begin() + hi);
+		uint64_t bytes = 0;
+		for (auto& x : d) {
+			x.out_cap = slot_cap(x, block_max);
+			x.out_off = bytes + uint64_t(HISTORY_SIZE);
+			bytes += uint64_t(HISTORY_SIZE) + round256(x.out_cap);
+		}
+		struct {
+			uint8_t* p;
+		} bx{ scratch(SC_X, size_t(bytes)) }, by{ bx.p ? scratch(SC_Y, size_t(bytes)) : nullptr },
+		    bh{ by.p ? scratch(SC_H, size_t(bytes)) : nullptr },
+		    tab{ bh.p ? scratch(SC_TAB, index_table_bytes(frame_len, nb)) : nullptr };
+		if (!tab.p) {
+			if (budget > (uint64_t(64) << 20) && nb > 1) {
+				budget /= 2;
+				continue;
+			}
+			return BULK_EXACT;
+		}
+		DevBuf<lz4ada_block_desc> d_desc;
+		DevBuf<lz4ada_block_status> sx, sy, sh;
+		d_desc.reserve(nb);
+		sx.reserve(nb);
+		sy.reserve(nb);
+		sh.reserve(nb);
+		const size_t sb = nb * sizeof(lz4ada_block_status);
+		phase("alloc");
+		HIP_OK(hipMemcpyAsync(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc),
+		                      hipMemcpyHostToDevice, stream));
+		HIP_OK(hipMemsetAsync(sx.p, 0, sb, stream));
+		HIP_OK(launch_link_fill(bx.p, by.p, bh.p, d_desc.p, nb, stream));
+		HIP_OK(launch_block_checksums(d_frame, d_desc.p, nb, sx.p, stream));
+		HIP_OK(launch_index(d_frame, frame_len, d_desc.p, nb, tab.p, sx.p, stream));
+		HIP_OK(hipMemcpyAsync(sy.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
+		HIP_OK(hipMemcpyAsync(sh.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
+		uint8_t* bufs[3] = { bx.p, by.p, bh.p };
+		lz4ada_block_status* sts[3] = { sx.p, sy.p, sh.p };
+		for (int k = 0; k < 3; ++k) {
+			HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bufs[k], sts[k], 2,
+			                             stream));
+			HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bufs[k], sts[k], 1, LINK_HIST,
+			                        stream));
+		}
+		phase("decodes");
+		std::vector<lz4ada_block_status> st(nb);
+		d2h(st.data(), sx.p, sb, stream);
+		std::vector<int64_t> A(nb);
+		int64_t n = 0;
+		const int64_t opos0 = opos, oph0 = oph;  // this batch's start (a smaller retry rescans)
+		// the first block the exact path has to take: a block error, a
+		// checksum mismatch, or quirk D1 (a match reaching
+		// >= D1_OFF back into the history right after a block that ended at
+		// 65536..65542).  The blocks before it only point backwards, so they
+		// resolve on their own and the exact path resumes at it.
+		uint32_t ok_n = nb;
+		for (uint32_t i = 0; i < nb; ++i) {
+			if (opos >= HISTORY_SIZE)
+				opos = 0;
+			if (st[i].code != DS_OK ||
+			    ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum) ||
+			    ((st[i].aux & AUX_D1_RISK) && oph >= HISTORY_SIZE && oph <= HISTORY_SIZE + 6)) {
+				ok_n = i;
+				break;
+			}
+			opos += st[i].out_len;
+			if (opos >= HISTORY_SIZE)
+				oph = opos;
+			A[i] = n;
+			n += st[i].out_len;
+		}
+		if (ok_n < nb) {
+			fail = int64_t(lo) + ok_n;
+			nb = ok_n;
+			if (nb == 0)
+				return BULK_FAIL_AT;
+		}
+		if (n >= (int64_t(1) << 31) - HISTORY_SIZE) {  // words hold positions + 65536 in 31 bits
+			if (nb > 1) {
+				// the smaller batch rescans from this batch's start: its own
+				// first failing block (if any) and the replayed positions
+				budget /= 2;
+				fail = -1;
+				opos = opos0;
+				oph = oph0;
+				continue;
+			}
+			return BULK_EXACT;
+		}
+		DevBuf<int64_t> d_A;
+		DevBuf<uint32_t> d_ctr;
+		struct {
+			uint32_t* p;
+		} d_P{ reinterpret_cast<uint32_t*>(scratch(SC_P, size_t(std::max<int64_t>(n, 1)) * 4)) };
+		if (!d_P.p)
+			return BULK_EXACT;
+		d_A.reserve(nb);
+		d_ctr.reserve(2);
+		HIP_OK(hipMemcpyAsync(d_A.p, A.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+		HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
+		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
+		uint32_t ctr[2] = { 0, 0 };
+		uint8_t* F = nullptr;
+		// a word per output byte (resolving only the history-derived bytes,
+		// round 4's sparse form, measured slower -- three gathers per target
+		// instead of one word -- DESIGN §7)
+		{
+			// the constant bytes go to F with the words, each round writes the
+			// bytes it resolves: the last round leaves the output
+			F = sink.dst(n);
+			if (!F)
+				return BULK_EXACT;
+			// span activity flags, double-buffered across rounds (an init that
+			// also stepped every history-derived byte one pointer forward was
+			// measured and dropped: mixed 10.32 vs 10.35 ms, chain 13.5 vs
+			// 15.4, dense 31.0 vs 23.7 -- its byte gathers cost what the round
+			// saves)
+			const int64_t ns = link_spans(n);
+			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
+			if (!act)
+				return BULK_EXACT;
+			// init flags the spans that hold a history-derived byte: the
+			// first round reads only those
+			HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
+			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
+			                        act + ns, d_ctr.p, stream));
+			d2h(ctr, d_ctr.p, sizeof ctr, stream);
+			phase("init");
+			for (int round = 0; ctr[0] > 0; ++round) {
+				if (round > 64)
+					return BULK_EXACT;  // never expected: every pointer goes strictly back
+				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
+				uint8_t* a_out = act + (round & 1) * ns;
+				const uint8_t* a_in = act + ((round + 1) & 1) * ns;
+				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out, d_ctr.p,
+				                        stream));
+				d2h(ctr, d_ctr.p, sizeof ctr, stream);
+				if (ctr[1])
+					return BULK_EXACT;  // a reference before the frame start: the exact error
+			}
+			phase("jumps");
+		}
+		HIP_OK(launch_link_tail(F, n, d_tail[cur].p, d_tail[cur ^ 1].p, stream));
+		cur ^= 1;
+		phase("emit");
+		sink.done(F, n);
+		phase("sink");
+		total += uint64_t(n);
+		for (uint32_t i = 0; i < nb; ++i)
+			lens.push_back(st[i].out_len);
+		if (fail >= 0)
+			return BULK_FAIL_AT;
+		lo = hi;
+	}
+	return BULK_OK;
+}
+
+}  // namespace lz4ada

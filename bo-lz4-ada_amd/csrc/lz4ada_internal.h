@@ -1,4 +1,4 @@
-// lz4ada_internal.h -- types shared by the host frame engine (lz4ada_host.cpp)
+// lz4ada_internal.h -- types shared by the host units (lz4ada_host_common.h, lz4ada_facade.cpp, lz4ada_bulk.cpp, lz4ada_bulk_linked.cpp)
 // and the gfx950 kernels (lz4ada_kernels.hip).  Not part of the public C-ABI.
 #pragma once
 
@@ -202,7 +202,7 @@ hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap
 hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ada_block_status* d_st,
                                    void* d_scratch, hipStream_t stream, int32_t H);
 
-// host side (lz4ada_host.cpp): the calling thread's message for
+// host side (lz4ada_bulk.cpp): the calling thread's message for
 // lz4ada_thread_last_error() and its lz4ada_last_path() bits
 void set_thread_error(const std::string& msg);
 void set_last_path(int bits);

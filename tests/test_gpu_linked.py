@@ -110,7 +110,7 @@ def matches(payload):
 
 
 def d1_risk(blocks):
-    """Whether the host's D1 rule (lz4ada_host.cpp bulk_linked) must send the
+    """Whether the host's D1 rule (lz4ada_bulk_linked.cpp bulk_linked) must send the
     frame to the exact path: a block starting right after Output_Pos_History
     was set to 65536..65542 (lz4ada.adb:678-690, 785-787) with a match of
     offset >= 65529 reaching before the block start."""

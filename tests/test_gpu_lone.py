@@ -105,7 +105,7 @@ def test_lone_corrupted_blocks_never_differ(seed):
 
 
 # ------------------------------------------- frames of a few large blocks
-# (lz4ada_host.cpp few_large_blocks: decode_frame and the facade's read-ahead
+# (lz4ada_host_common.h few_large_blocks: decode_frame and the facade's read-ahead
 # take such frames one block at a time through the lone-block decoder)
 
 def few_block_frame(kinds, seed=9, stored_at=None):

@@ -50,7 +50,7 @@ def main():
                     help="decoded bytes per block (default: --block-max)")
     ap.add_argument("--dump", default="",
                     help="also write the frame and its expected output (path, path + '.out') "
-                         "for tools/facade_c (the same loop without Python)")
+                         "for bo-lz4-ada_amd/facade_bench (the same loop from C)")
     args = ap.parse_args()
     n = args.raw_len or args.block_max
     if args.indep:
