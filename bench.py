@@ -109,7 +109,9 @@ def kernel_code_hash(kernel: str = "k_decode_idx", lib: str = None) -> str:
     liblz4ada_hip.so, the code object's symbol table): profiles/pmc_decode.json
     records the hash it was measured with, and bench.py reports its traffic
     only while the hash still matches -- a change to that kernel's code or
-    resources voids the figure, a change elsewhere does not.  None when the
+    resources voids the figure, a change elsewhere does not (the descriptor's
+    code-entry offset, which moves when other kernels are added, is left
+    out).  None when the
     library or the kernel is not found."""
     import hashlib
     import struct
@@ -144,7 +146,10 @@ def kernel_code_hash(kernel: str = "k_decode_idx", lib: str = None) -> str:
                     name = elf[strtab[4] + nm:elf.index(b"\0", strtab[4] + nm)].decode(errors="replace")
                     if want in name and 0 < shndx < len(secs) and sz:
                         sec = secs[shndx]
-                        parts[name] = elf[sec[4] + val - sec[3]:sec[4] + val - sec[3] + sz]
+                        part = bytearray(elf[sec[4] + val - sec[3]:sec[4] + val - sec[3] + sz])
+                        if name.endswith(".kd") and len(part) >= 24:
+                            part[16:24] = bytes(8)  # kernel_code_entry_byte_offset: where the code lies
+                        parts[name] = bytes(part)
             if parts:
                 h = hashlib.sha256()
                 for name in sorted(parts):

@@ -925,17 +925,21 @@ struct alignas(16) DecLds {
 // The output window and per-wave scratch of an LDS layout: DecLds (one
 // wave per block) holds them directly; a two-wave block's view (W2, below)
 // picks its wave's scratch.
-__device__ __forceinline__ uint8_t (&oring_of(DecLds& D))[ORING] { return D.oring; }
-__device__ __forceinline__ const uint8_t (&oring_of(const DecLds& D))[ORING] { return D.oring; }
+__device__ __forceinline__ uint8_t* oring_of(DecLds& D) { return D.oring; }
+__device__ __forceinline__ const uint8_t* oring_of(const DecLds& D) { return D.oring; }
 __device__ __forceinline__ uint8_t* own_of(DecLds& D) { return D.own; }
 __device__ __forceinline__ uint64_t* ldesc_of(DecLds& D) { return D.ldesc; }
+// the window's size - 1 (a power of two) for a layout: ORING unless the
+// layout says otherwise (the pipelined pair's 16 KiB window)
+template <class LD>
+__device__ __forceinline__ constexpr uint32_t omask_of(const LD&) { return OMASK; }
 
 // Exact-length store of n (1..16) bytes at output position x into the ring.
 template <class LD>
 __device__ __forceinline__ void ostore(LD& L, int32_t x, u32x4 v, int32_t n)
 {
-	const uint32_t a = uint32_t(x) & OMASK;
-	if (a + uint32_t(n) <= uint32_t(ORING)) {
+	const uint32_t a = uint32_t(x) & omask_of(L);
+	if (a + uint32_t(n) <= omask_of(L) + 1) {
 		// one ds_write_b128 even when misaligned: 256 cycles against 1579
 		// for four ds_write_b32 (each misaligned one is split too) and 384
 		// for 16 ds_write_b8 (tools/lds_bench.hip, dependent chain)
@@ -946,14 +950,14 @@ __device__ __forceinline__ void ostore(LD& L, int32_t x, u32x4 v, int32_t n)
 	const uint64_t hi = uint64_t(v.z) | (uint64_t(v.w) << 32);
 	for (int32_t i = 0; i < n; ++i) {
 		const uint64_t w = i < 8 ? lo : hi;
-		oring_of(L)[(a + uint32_t(i)) & OMASK] = uint8_t(w >> (8 * (i & 7)));
+		oring_of(L)[(a + uint32_t(i)) & omask_of(L)] = uint8_t(w >> (8 * (i & 7)));
 	}
 }
 
 template <class LD>
 __device__ __forceinline__ u32x4 oload16(const LD& L, int32_t x)
 {
-	return ring16(oring_of(L), uint32_t(x) & OMASK, OMASK);
+	return ring16(oring_of(L), uint32_t(x) & omask_of(L), omask_of(L));
 }
 
 // Store steps and phases of period-off patterns without integer division:
@@ -1097,19 +1101,21 @@ __device__ __forceinline__ int32_t chunk_owner(LD& D, int32_t inc, int32_t np, i
 
 // chunk_owner over two rounds' entries (round 0's lanes, then round 1's:
 // entry 64 r + lane holds pieces [inc_r - np_r, inc_r)), owner 0..127.
-__device__ __forceinline__ int32_t chunk_owner2(DecLds& D, int32_t inc0, int32_t np0, int32_t inc1,
+template <class LD>
+__device__ __forceinline__ int32_t chunk_owner2(LD& D, int32_t inc0, int32_t np0, int32_t inc1,
                                                 int32_t np1, int32_t t0)
 {
 	const int32_t lane = int32_t(lane_id());
 	const int32_t seed = __popcll(__ballot(inc0 <= t0)) + __popcll(__ballot(inc1 <= t0));
-	D.own[lane] = uint8_t(lane == 0 ? seed : 0);
+	uint8_t* own = own_of(D);
+	own[lane] = uint8_t(lane == 0 ? seed : 0);
 	const int32_t e0 = inc0 - np0, e1 = inc1 - np1;
 	if (np0 > 0 && e0 >= t0 && e0 < t0 + 64)
-		D.own[e0 - t0] = uint8_t(lane);
+		own[e0 - t0] = uint8_t(lane);
 	if (np1 > 0 && e1 >= t0 && e1 < t0 + 64)
-		D.own[e1 - t0] = uint8_t(64 + lane);
+		own[e1 - t0] = uint8_t(64 + lane);
 	wave_lds_fence();
-	const int32_t v = D.own[lane];
+	const int32_t v = own[lane];
 	wave_lds_fence();  // own[] is marked again for the next chunk
 	return wave_incl_max(v);
 }
@@ -1136,7 +1142,8 @@ __device__ __forceinline__ int32_t match_pieces(int32_t off, int32_t ml)
 // Both rounds' ring-sourced matches (round r: mdst[r], off[r], ml[r]; ml 0:
 // none), dealt together in output order; a piece finds its match in an LDS
 // descriptor (D.ldesc, free after the literals) instead of by shuffles.
-__device__ __forceinline__ int32_t ring_pieces(DecLds& D, const int32_t (&mdst)[RMAX],
+template <class LD>
+__device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX],
                                                const int32_t (&off)[RMAX], const int32_t (&ml)[RMAX],
                                                int32_t o_batch)
 {
@@ -1151,8 +1158,9 @@ __device__ __forceinline__ int32_t ring_pieces(DecLds& D, const int32_t (&mdst)[
 		return uint64_t(uint16_t(md - o_batch)) | (uint64_t(uint16_t(of)) << 16) |
 		       (uint64_t(uint16_t(m)) << 32) | (uint64_t(uint16_t(excl)) << 48);
 	};
-	D.ldesc[lane] = pack(mdst[0], off[0], ml[0], inc0 - np0);
-	D.ldesc[64 + lane] = pack(mdst[1], off[1], ml[1], inc1 - np1);
+	uint64_t* ldesc = ldesc_of(D);
+	ldesc[lane] = pack(mdst[0], off[0], ml[0], inc0 - np0);
+	ldesc[64 + lane] = pack(mdst[1], off[1], ml[1], inc1 - np1);
 	for (int32_t t0 = 0; t0 < tot; t0 += 64) {
 		const int32_t t = t0 + lane;
 		const bool act = t < tot;
@@ -1161,7 +1169,7 @@ __device__ __forceinline__ int32_t ring_pieces(DecLds& D, const int32_t (&mdst)[
 #else
 		const int32_t lo = min(chunk_owner2(D, inc0, np0, inc1, np1, t0), 127);
 #endif
-		const uint64_t dd = D.ldesc[lo];
+		const uint64_t dd = ldesc[lo];
 		const int32_t od = o_batch + int32_t(dd & 0xffffu);
 		const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
 		const int32_t k = t - int32_t(dd >> 48);
@@ -2069,8 +2077,8 @@ struct W2 {
 	DecLds2& L;
 	int32_t w;
 };
-__device__ __forceinline__ uint8_t (&oring_of(W2& V))[ORING] { return V.L.oring; }
-__device__ __forceinline__ const uint8_t (&oring_of(const W2& V))[ORING] { return V.L.oring; }
+__device__ __forceinline__ uint8_t* oring_of(W2& V) { return V.L.oring; }
+__device__ __forceinline__ const uint8_t* oring_of(const W2& V) { return V.L.oring; }
 __device__ __forceinline__ uint8_t* own_of(W2& V) { return V.L.own[V.w]; }
 __device__ __forceinline__ uint64_t* ldesc_of(W2& V) { return V.L.ldesc[V.w]; }
 
@@ -2537,6 +2545,610 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 
+
+// ============================================================ pipelined pair
+// k_decode_pp2 (round 5): two waves per block that pipeline consecutive
+// batches instead of splitting each one (k_decode_idx2), for launches of at
+// most one block per SIMD -- a configs[3] shard at N = 8 (1,024 blocks) --
+// where a block has the LDS (~30 KiB) and the VGPRs (two waves per SIMD at
+// <= 256) for two-round batches of up to 128 sequences in each wave.  Each
+// block's chain is latency-bound: wave w takes batches j = w,
+// w + 2, ...; batch j's staging, cut, parse, HBM-sourced loads, literals and
+// HBM-sourced stores run while the other wave is still inside batch j - 1,
+// and only the ring-sourced matches (which may read batch j - 1's output)
+// wait for batch j - 1's to be stored -- an LDS token, no barrier in the
+// batch loop.  Both waves compute every cut from the staged pass-1 records
+// (each its own batch and the next), so they agree on the batch sequence,
+// on who stages which input chunk and on the HBM threshold; spin waits on
+// LDS counters carry the hand-offs, each bounded (a hand-off that never
+// comes declines the block instead of hanging the grid).
+//
+// Window discipline (16 KiB output window, batches of <= OW bytes): while
+// batch j runs its ring-sourced matches, batch j + 1 may write its literals
+// and HBM-sourced bytes, so the window keeps [o_j - RFLOOR2, o_j + OW)
+// intact.  A match reads HBM for its source bytes below glo_j =
+// align16(o_{j-1}) rounded down to a 128-byte line (written by the flushes
+// of batches <= j - 2, whose completion each wave publishes after its own
+// vmcnt wait; a CU's L1 never gets a line holding bytes not yet flushed) in
+// whole 16-byte pieces, and the window for the rest (a match straddling the
+// threshold is split in two).  A first try with one-round batches and four
+// waves per SIMD at 2,048 blocks (k_decode_pp, commit dd280ab) ran 15.6 ms
+// against k_decode_idx's 13.3: 64-sequence batches cost ~0.7 of a
+// 128-sequence one (tools/time_decode.py, LZ4ADA_SEQ_CUT=64), and four
+// waves per SIMD slow each one ~1.3x.
+
+constexpr int ORING2 = 16384;                 // output window of the pipelined pair
+constexpr int32_t RFLOOR2 = ORING2 - 2 * OW;  // window bytes kept below a batch through its ring phase
+static_assert(OW + 16 + 128 + 16 < RFLOOR2, "the HBM threshold must lie inside the kept window");
+
+struct alignas(16) PpLds2 {
+	uint8_t ring[RING + 16];   // staged input: 4 chunks of 2 KiB (+ mirror), shared
+	uint8_t oring[ORING2];     // output window, shared
+	uint64_t rrec[4 * 64];     // pass-1 records of the staged chunks
+	uint64_t ldesc[2][2 * 64]; // per wave: run / match descriptors of both rounds
+	uint16_t cst[2][MAXSEQ];   // per wave: its batch's sequence starts
+	uint8_t own[2][256];       // per wave: piece owners
+	int32_t tok;               // last batch whose ring-sourced matches are stored
+	int32_t staged;            // input chunks staged so far
+	int32_t abort_;            // a wave declined the block
+	int32_t pad;
+	int32_t done[2];           // per wave: last own batch whose flush has completed
+};
+
+struct WP2 {
+	PpLds2& L;
+	int32_t w;
+};
+__device__ __forceinline__ uint8_t* oring_of(WP2& V) { return V.L.oring; }
+__device__ __forceinline__ const uint8_t* oring_of(const WP2& V) { return V.L.oring; }
+__device__ __forceinline__ uint8_t* own_of(WP2& V) { return V.L.own[V.w]; }
+__device__ __forceinline__ uint64_t* ldesc_of(WP2& V) { return V.L.ldesc[V.w]; }
+__device__ __forceinline__ constexpr uint32_t omask_of(const WP2&) { return ORING2 - 1; }
+
+__device__ __forceinline__ int32_t lds_peek(const int32_t* p)
+{
+	return __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile int32_t*>(p));
+}
+
+// Publish v at p after every LDS write of this wave so far (the other wave
+// reads those once it sees v): lgkmcnt(0) only, the flush stores in flight
+// are not waited for.
+__device__ __forceinline__ void lds_publish(int32_t* p, int32_t v)
+{
+	asm volatile("" ::: "memory");
+	__builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
+	*reinterpret_cast<volatile int32_t*>(p) = v;
+	asm volatile("" ::: "memory");
+}
+
+// Wait until *p >= want; false if the block was aborted meanwhile -- or
+// after ~2^24 polls (~0.5 s): a hand-off that never comes declines the
+// block (DS_RETRY: k_decode_pc redoes it) instead of hanging the grid.
+__device__ __forceinline__ bool lds_wait_ge(int32_t* abort_flag, const int32_t* p, int32_t want)
+{
+	for (uint32_t it = 0; lds_peek(p) < want; ++it) {
+		if (lds_peek(abort_flag))
+			return false;
+		if (it >= (1u << 24)) {
+			lds_publish(abort_flag, 1);
+			return false;
+		}
+		__builtin_amdgcn_s_sleep(1);
+	}
+	asm volatile("" ::: "memory");
+	return true;
+}
+
+// One batch cut from the staged records (decode_block's rule: <= OW output
+// bytes, <= MAXSEQ sequences): sub-segments [k0, k0 + m).  over: the first
+// sub-segment alone exceeds a limit -- the 64 from k0 go straight to HBM.
+struct PpCut {
+	int32_t m, bytes;
+	bool over;
+};
+__device__ __forceinline__ PpCut pp_cut(const PpLds2& L, int32_t k0, int32_t nsub)
+{
+	const int32_t k = k0 + int32_t(lane_id());
+	const uint64_t rec = k < nsub ? L.rrec[k & 255] : 0;
+	const int32_t cnt = int32_t(min(uint32_t(rec >> 32), 1u << 24));
+	const int32_t incl = wave_incl_scan(cnt);
+	const int32_t incl_s = wave_incl_scan(__popc(uint32_t(rec)));
+	PpCut c;
+	c.m = __popcll(__ballot(incl <= OW && incl_s <= MAXSEQ));
+	c.over = c.m == 0;
+	c.m = c.over ? 64 : c.m;
+	c.bytes = __shfl(incl, c.m - 1);
+	return c;
+}
+
+__device__ __forceinline__ void pp_load_chunk(uintptr_t abase, int32_t c, uintptr_t lim, const uint64_t* tab,
+                                              int32_t nsub, u32x4& v0, u32x4& v1, uint64_t& r)
+{
+	load_chunk2(abase, c, lim, v0, v1);
+	const int32_t k = 64 * c + int32_t(lane_id());
+	r = k < nsub ? __builtin_nontemporal_load(tab + k) : 0;
+}
+
+__device__ __forceinline__ void pp_stage_chunk(PpLds2& L, int32_t c, const u32x4& v0, const u32x4& v1,
+                                               uint64_t r)
+{
+	const uint32_t lane = lane_id();
+	const uint32_t a = uint32_t(c * BATCH) & (RING - 1);
+	*reinterpret_cast<u32x4*>(&L.ring[a + 16 * lane]) = v0;
+	*reinterpret_cast<u32x4*>(&L.ring[a + 1024 + 16 * lane]) = v1;
+	if (a == 0 && lane == 0)
+		*reinterpret_cast<u32x4*>(&L.ring[RING]) = v0;
+	L.rrec[64 * (c & 3) + lane] = r;
+}
+
+// Pass 2 of block b (independent; pass 1's verdict DS_OK) by both waves.
+// Returns the output length, or -1 when the block is declined.
+__device__ __forceinline__ int32_t decode_block_pp2(PpLds2& L, const uint8_t* __restrict__ frame,
+                                                    uint64_t frame_len,
+                                                    const lz4ada_block_desc* __restrict__ desc, uint32_t b,
+                                                    const uint8_t* __restrict__ tab_all,
+                                                    uint8_t* __restrict__ out)
+{
+	const int32_t tid = int32_t(threadIdx.x), w = tid >> 6, lane = tid & 63;
+	WP2 V{ L, w };
+	const lz4ada_block_desc d = desc[b];
+	cg8* in = gptr(frame) + d.in_off;
+	g8* ob = gptr(out) + d.out_off;
+	const int32_t n = int32_t(d.in_len);
+	const int32_t cap = int32_t(d.out_cap);
+	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
+	const uintptr_t olim = reinterpret_cast<uintptr_t>(ob) + uintptr_t(cap);
+	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+	const uint64_t* tab = reinterpret_cast<const uint64_t*>(tab_all) + (((d.in_off >> 8) + b) << 3);
+	const int32_t nsub = (n + SUB - 1) / SUB;
+	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
+	constexpr uint32_t WMASK = ORING2 - 1;
+	int32_t* const abort_flag = &L.abort_;
+
+	Src S;
+	S.lds = L.ring;
+	S.mask = RING - 1;
+	S.mis = mis;
+	S.in = in;
+	S.lim = lim;
+
+	// The cut cursor: the next batch to cut is j, at sub-segment k0 and
+	// output byte o; hi = input chunks staged once the batches cut so far
+	// have staged theirs (the owner of batch j stages [hi_before, cf_j + 3)).
+	// o_prev / over_prev: batch j - 1's output start and whether it went
+	// straight to HBM.  Each wave cuts its own batch and the next one.
+	int32_t j = 0, k0 = 0, o = 0, hi = 0, o_prev = 0;
+	bool over_prev = false;
+	auto advance = [&](PpCut& c) {
+		c = pp_cut(L, k0, nsub);
+		o_prev = o;
+		over_prev = c.over;
+		o += c.bytes;
+		k0 += c.m;
+		++j;
+	};
+	auto chunk_of = [&](int32_t k) { return (k * SUB + mis) / BATCH; };
+	u32x4 pf0 = u32x4{ 0u, 0u, 0u, 0u }, pf1 = pf0;  // this wave's prefetched chunk pfc
+	uint64_t pr = 0;
+	int32_t pfc = -1;
+	bool bad = false;
+	if (w == 1 && k0 < nsub) {  // batch 0 is wave 0's: cut it once staged
+		hi = chunk_of(0) + 3;
+		PpCut c0;
+		if (lds_wait_ge(abort_flag, &L.staged, hi))
+			advance(c0);
+		else
+			bad = true;
+	}
+
+	while (!bad && k0 < nsub) {
+		// ---- batch j is this wave's
+		const int32_t jb = j, ob0 = o, kb = k0;
+		const bool prev_over = over_prev;
+		// HBM holds, complete, every byte below glo: batches <= j - 2, or all
+		// of batch j - 1 when it went straight to HBM
+		const int32_t glo = jb == 0 ? 0 : ((prev_over ? ob0 : o_prev) & ~15);
+		const int32_t cf = chunk_of(kb);
+		const int32_t hi_before = hi;
+		hi = max(hi, cf + 3);
+		if (!lds_wait_ge(abort_flag, &L.staged, hi_before)) {
+			bad = true;
+			break;
+		}
+		for (int32_t c = hi_before; c < hi; ++c) {
+			if (c != pfc) {
+				pp_load_chunk(abase, c, lim, tab, nsub, pf0, pf1, pr);
+				__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a rare path's loads settle here
+			}
+			pp_stage_chunk(L, c, pf0, pf1, pr);
+			pfc = -1;
+		}
+		if (hi > hi_before)
+			lds_publish(&L.staged, hi);
+		S.lo = cf * BATCH - mis;
+		S.hi = hi * BATCH - mis;
+		// this batch's cut, then the next one's (its records are staged:
+		// chunks <= cf + 2), which places this wave's next batch: prefetch the
+		// chunk that batch will stage
+		PpCut cb;
+		advance(cb);
+		const int32_t oe = o;
+		bool next_over = false;
+		int32_t npf = 0;  // vector loads issued after this wave's last flush
+		if (k0 < nsub) {
+			hi = max(hi, chunk_of(k0) + 3);
+			PpCut cn;
+			advance(cn);
+			next_over = cn.over;
+			if (k0 < nsub && chunk_of(k0) + 3 > hi) {
+				pfc = hi;
+				pp_load_chunk(abase, pfc, lim, tab, nsub, pf0, pf1, pr);
+				npf = 3;
+			}
+		}
+		if (oe > cap) {
+			bad = true;
+			lds_publish(abort_flag, 1);
+			break;
+		}
+		if (cb.over) {
+			// ---- a sub-segment alone exceeds the batch limits: the 64
+			// sub-segments go straight to HBM (batch_global), alone -- after
+			// every earlier batch's bytes are final in HBM and in the window
+			if (!lds_wait_ge(abort_flag, &L.tok, jb - 1) || !lds_wait_ge(abort_flag, &L.done[w ^ 1], jb - 1)) {
+				bad = true;
+				break;
+			}
+			vm_wait();
+			const int32_t k = kb + lane;
+			const int32_t sub_s = k * SUB;
+			const int32_t sub_end = min(sub_s + SUB, n);
+			const uint64_t rec = (k < nsub) ? L.rrec[k & 255] : 0;
+			const uint32_t bm = uint32_t(rec);
+			const int32_t cnt = int32_t(min(uint32_t(rec >> 32), 1u << 24));
+			const int32_t p0 = bm ? sub_s + __builtin_ctz(bm) : n;
+			const int32_t incl = wave_incl_scan(cnt);
+			const int32_t a0 = ob0 & ~15;
+			if (lane == 0 && ob0 > a0)  // the window's unflushed tail
+				gstore_n(ob + a0, *reinterpret_cast<const u32x4*>(&L.oring[a0 & WMASK]), ob0 - a0);
+			vm_wait();
+			const bool ok = !__any(!batch_global(S, ob, olim, p0, sub_end, n, ob0 + incl - cnt, ob0, 0));
+			vm_wait();
+			if (!ok) {
+				bad = true;
+				lds_publish(abort_flag, 1);
+				break;
+			}
+			// the window's history again, from HBM (nontemporal: past the L1,
+			// which may hold lines of this batch from before their stores)
+			const int32_t x0 = max(oe - ORING2 + 16, 0) & ~15;
+			for (int32_t x = x0 + 16 * lane; x < oe + 15; x += 64 * 16)
+				*reinterpret_cast<u32x4*>(&L.oring[uint32_t(x) & WMASK]) =
+				    x + 16 <= cap ? __builtin_nontemporal_load(reinterpret_cast<const GLOBAL u32x4*>(ob + x))
+				                  : gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(intptr_t(x)), olim);
+			__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+			lds_publish(&L.done[w], jb);
+			lds_publish(&L.tok, jb);
+			continue;
+		}
+		if (prev_over && !lds_wait_ge(abort_flag, &L.tok, jb - 1)) {
+			bad = true;  // (the batch before went straight to HBM: its window reload first)
+			break;
+		}
+
+		// ---- the batch's sequence starts, in output order
+		const int32_t base = kb * SUB;
+		int32_t N;
+		{
+			const int32_t k = kb + lane;
+			const int32_t sub_s = k * SUB;
+			const uint64_t rec = (k < nsub) ? L.rrec[k & 255] : 0;
+			uint32_t bm = uint32_t(rec);
+			const int32_t nseq = __popc(bm);
+			const int32_t incl_s = wave_incl_scan(nseq);
+			if (lane < cb.m) {
+				int32_t e = incl_s - nseq;
+				const uint16_t rel = uint16_t(sub_s - base);
+				for (; bm; bm &= bm - 1)
+					L.cst[w][e++] = uint16_t(rel + __builtin_ctz(bm));
+			}
+			N = __shfl(incl_s, cb.m - 1);
+		}
+		wave_lds_fence();
+		const int32_t gl = glo & ~127;  // HBM pieces end in whole lines below this
+
+		// ---- P: up to 64 sequences per round, placed by a prefix sum; each
+		// match split into its HBM part (hml bytes) and its window part
+		int32_t rL[RMAX], rlit[RMAX], roff[RMAX], rml[RMAX], rdst[RMAX], rbeg[RMAX], hml[RMAX];
+		bool pre = false, anyg = false;
+		{
+			int32_t o_round = ob0;
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				rL[r] = rlit[r] = roff[r] = rml[r] = hml[r] = 0;
+				rbeg[r] = o_round;
+				if (64 * r < N) {
+					const int32_t idx = 64 * r + lane;
+					if (idx < N) {
+						Seq q;
+						parse_fast(S, base + int32_t(L.cst[w][idx]), n, q);
+						rL[r] = q.L;
+						rlit[r] = q.lit;
+						roff[r] = q.off;
+						rml[r] = q.ml;
+					}
+					const int32_t len = rL[r] + rml[r];
+					const int32_t inc = wave_incl_scan(len);
+					rdst[r] = o_round + inc - len;
+					o_round += __shfl(inc, 63);
+					const int32_t mdst = rdst[r] + rL[r];
+					if (rml[r] > 0) {
+						if (roff[r] > mdst)
+							pre = true;  // a reference before the block start (D2)
+						const int32_t room = gl - (mdst - roff[r]);
+						hml[r] = ((rml[r] + 15) & ~15) <= room ? rml[r] : max(room & ~15, 0);
+						if (hml[r] > 0)
+							anyg = true;
+					}
+				}
+			}
+		}
+		if (__any(pre)) {
+			bad = true;
+			lds_publish(abort_flag, 1);
+			break;
+		}
+
+		// ---- HBM-sourced parts: this wave's flush of batch j - 2 first (the
+		// prefetch loads issued after it may stay in flight), then the other
+		// wave's of batch j - 3; every load in flight before the first use: a
+		// part's first piece in its own lane, the rest of both rounds dealt
+		if (npf)
+			asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+		else
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		lds_publish(&L.done[w], max(jb - 2, -1));
+		u32x4 vg[RMAX], vr = u32x4{ 0u, 0u, 0u, 0u };
+		int32_t rtot[RMAX], rfirst[RMAX];
+		int32_t rpd = 0, rpn = 0;
+#pragma unroll
+		for (int r = 0; r < RMAX; ++r) {
+			vg[r] = vr;
+			rtot[r] = rfirst[r] = 0;
+		}
+		if (__any(anyg)) {
+			if (!lds_wait_ge(abort_flag, &L.done[w ^ 1], jb - 3)) {
+				bad = true;
+				break;
+			}
+			int32_t nc[RMAX];
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				nc[r] = 0;
+				if (64 * r < N) {
+					const int32_t src = rdst[r] + rL[r] - roff[r];
+					if (hml[r] > 0)
+						__builtin_memcpy(&vg[r], ob + src, 16);
+					nc[r] = hml[r] > 0 ? max(((hml[r] + 15) >> 4) - 1, 0) : 0;
+				}
+			}
+			if (__any(nc[0] > 0 || nc[1] > 0)) {
+				const int32_t inc0 = wave_incl_scan(nc[0]);
+				const int32_t tot0 = __shfl(inc0, 63);
+				const int32_t inc1 = tot0 + wave_incl_scan(nc[1]);
+				const int32_t tot = __shfl(inc1, 63);
+				rtot[0] = tot0;
+				rtot[1] = tot - tot0;
+				rfirst[0] = 64;
+				rfirst[1] = max(64 - tot0, 0);
+				auto pack = [&](int32_t md, int32_t of, int32_t m, int32_t excl) -> uint64_t {
+					return uint64_t(uint16_t(md - ob0)) | (uint64_t(uint16_t(of)) << 16) |
+					       (uint64_t(uint16_t(m)) << 32) | (uint64_t(uint16_t(excl)) << 48);
+				};
+				uint64_t* ldesc = ldesc_of(V);
+				ldesc[lane] = pack(rdst[0] + rL[0], roff[0], hml[0], inc0 - nc[0]);
+				ldesc[64 + lane] = pack(rdst[1] + rL[1], roff[1], hml[1], inc1 - nc[1]);
+				const int32_t lo = min(chunk_owner2(V, inc0, nc[0], inc1, nc[1], 0), 127);
+				const uint64_t dd = ldesc[lo];
+				const int32_t od = ob0 + int32_t(dd & 0xffffu);
+				const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
+				const int32_t k = 1 + lane - int32_t(dd >> 48);
+				if (lane < tot) {
+					rpd = od + 16 * k;
+					rpn = min(16, oml - 16 * k);
+					__builtin_memcpy(&vr, ob + (od - ooff) + 16 * k, 16);
+				}
+				wave_lds_fence();  // ldesc / own are written again later
+			}
+		}
+
+		// ---- L: literals (input ring -> window), first pieces in-lane, the
+		// rest of both rounds dealt
+		{
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r)
+				if (rL[r] > 0)
+					ostore(V, rdst[r], fetch16(S, rlit[r]), min(16, rL[r]));
+			const int32_t nc0 = rL[0] > 16 ? (rL[0] - 1) >> 4 : 0;
+			const int32_t nc1 = rL[1] > 16 ? (rL[1] - 1) >> 4 : 0;
+			if (__any(nc0 > 0 || nc1 > 0)) {
+				const int32_t inc0 = wave_incl_scan(nc0);
+				const int32_t tot0 = __shfl(inc0, 63);
+				const int32_t inc1 = tot0 + wave_incl_scan(nc1);
+				const int32_t tot = __shfl(inc1, 63);
+				auto pack = [&](int32_t lit, int32_t dst, int32_t Lx, int32_t excl) -> uint64_t {
+					return uint64_t(uint16_t(lit - base)) | (uint64_t(uint16_t(dst - ob0)) << 16) |
+					       (uint64_t(uint16_t(Lx)) << 32) | (uint64_t(uint16_t(excl)) << 48);
+				};
+				uint64_t* ldesc = ldesc_of(V);
+				ldesc[lane] = pack(rlit[0], rdst[0], rL[0], inc0 - nc0);
+				ldesc[64 + lane] = pack(rlit[1], rdst[1], rL[1], inc1 - nc1);
+				for (int32_t t0 = 0; t0 < tot; t0 += 64) {
+					const int32_t t = t0 + lane;
+					const int32_t lo = min(chunk_owner2(V, inc0, nc0, inc1, nc1, t0), 127);
+					const uint64_t dd = ldesc[lo];
+					const int32_t lit = base + int32_t(dd & 0xffffu);
+					const int32_t dst = ob0 + int32_t((dd >> 16) & 0xffffu);
+					const int32_t Lx = int32_t((dd >> 32) & 0xffffu);
+					const int32_t k = 1 + t - int32_t(dd >> 48);
+					if (t < tot)
+						ostore(V, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, Lx - 16 * k));
+				}
+			}
+		}
+		wave_lds_fence();
+
+		// ---- M: the HBM-sourced parts (sources in HBM: no order among them)
+		int32_t mring[RMAX], oring[RMAX], lring[RMAX];
+		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+		if (rpn > 0)
+			ostore(V, rpd, vr, rpn);
+#pragma unroll
+		for (int r = 0; r < RMAX; ++r) {
+			mring[r] = oring[r] = lring[r] = 0;
+			if (64 * r < N) {
+				const int32_t mdst = rdst[r] + rL[r];
+				if (hml[r] > 0)
+					ostore(V, mdst, vg[r], min(16, hml[r]));
+				if (rtot[r] > rfirst[r]) {  // rare: more than 64 dealt pieces; the rest now
+					const int32_t nc = hml[r] > 0 ? max(((hml[r] + 15) >> 4) - 1, 0) : 0;
+					const int32_t inc = wave_incl_scan(nc);
+					for (int32_t t0 = rfirst[r]; t0 < rtot[r]; t0 += 64) {
+						const int32_t t = t0 + lane;
+						const int32_t lo = piece_owner(inc, t);
+						const int32_t k = 1 + t - (__shfl(inc, lo) - __shfl(nc, lo));
+						const int32_t osrc = __shfl(mdst - roff[r], lo), odst = __shfl(mdst, lo);
+						const int32_t oml = __shfl(hml[r], lo);
+						if (t < rtot[r]) {
+							u32x4 v;
+							__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
+							ostore(V, odst + 16 * k, v, min(16, oml - 16 * k));
+						}
+					}
+					__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+				}
+				// the window part: the match's bytes from hml on
+				mring[r] = mdst + hml[r];
+				oring[r] = roff[r];
+				lring[r] = rml[r] - hml[r];
+			}
+		}
+		wave_lds_fence();
+
+		// ---- window-sourced matches, after batch j - 1's
+		if (!lds_wait_ge(abort_flag, &L.tok, jb - 1)) {
+			bad = true;
+			break;
+		}
+		static_assert(RMAX == 2, "ring dealing pairs two rounds");
+		if (__any(lring[0] > RING_LANE_MAX || lring[1] > RING_LANE_MAX)) {
+			ring_pieces(V, mring, oring, lring, ob0);
+		} else {
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r)
+				if (64 * r < N)
+					ring_lanes(V, mring[r], oring[r], lring[r], rbeg[r], rL[r]);
+		}
+		lds_publish(&L.tok, jb);
+
+		// ---- flush whole 16-byte units of [ob0, oe) (the first may start
+		// before ob0: batch j - 1's bytes, final since its token)
+		{
+			const int32_t u0 = ob0 >> 4, u1 = oe >> 4;
+#pragma unroll
+			for (int i = 0; i < FLUSH_ST; ++i) {
+				const int32_t u = u0 + lane + 64 * i;
+				if (u < u1)
+					*reinterpret_cast<GLOBAL u32x4*>(ob + (u << 4)) =
+					    *reinterpret_cast<const u32x4*>(&L.oring[(u << 4) & WMASK]);
+			}
+		}
+		if (next_over) {
+			// the next batch goes straight to HBM once this flush is complete
+			vm_wait();
+			lds_publish(&L.done[w], jb);
+		}
+	}
+	// the last partial unit (after both waves' batches), by wave 0
+	__syncthreads();
+	bad = bad || lds_peek(abort_flag) != 0;
+	if (!bad && tid == 0 && (o & 15))
+		gstore_n(ob + (o & ~15), *reinterpret_cast<const u32x4*>(&L.oring[(o & ~15) & WMASK]), o & 15);
+	return bad ? -1 : o;
+}
+
+// Independent blocks, both passes, two waves per block pipelining batches
+// (pass 1: index_block2, both waves walking each chunk).  Two waves per SIMD
+// (<= 256 VGPRs; the block checksum kernel's 118 still fit beside them at
+// one block per SIMD).
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_pp2(
+        const uint8_t* __restrict__ frame, uint64_t frame_len, const lz4ada_block_desc* __restrict__ desc,
+        uint32_t nblocks, uint8_t* __restrict__ tab_all, uint8_t* __restrict__ out,
+        lz4ada_block_status* __restrict__ status)
+{
+	__shared__ union {
+		PpLds2 d;
+		IdxLds2 x;
+	} U;
+	if (blockIdx.x >= nblocks)
+		return;
+	const uint32_t b = blockIdx.x;
+	const int32_t tid = int32_t(threadIdx.x), w = tid >> 6;
+	index_block2(U.x, frame, frame_len, desc, b, tab_all, status);
+	// the table and status this block's pass 1 wrote are read back by both waves
+	vm_wait();
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+	__syncthreads();
+	const lz4ada_block_desc d = desc[b];
+	if (status[b].code != DS_OK)
+		return;  // declined: its status says so
+	if (d.flags & LZ4ADA_BLOCK_STORED) {
+		const int32_t n = int32_t(d.in_len);
+		int32_t c = DS_OK;
+		if (n > int32_t(d.out_cap)) {
+			c = DS_OUT_OVERFLOW;
+		} else {  // each wave copies half
+			Src S0;
+			S0.in = gptr(frame) + d.in_off;
+			S0.lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
+			const int32_t mid = (n >> 1) & ~1023;
+			const int32_t c0 = w == 0 ? 0 : mid, c1 = w == 0 ? mid : n;
+			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM)
+				wave_literal<0>(gptr(out) + d.out_off, c0, S0, c0, c1 - c0);
+			else
+				wave_literal<LZ4ADA_STORED_NT>(gptr(out) + d.out_off, c0, S0, c0, c1 - c0);
+		}
+		if (tid == 0) {
+			status[b].code = c;
+			status[b].aux = 0;
+			status[b].detail = 0;
+			status[b].err_out_pos = 0;
+			status[b].out_len = c == DS_OK ? uint32_t(n) : 0u;
+		}
+		return;
+	}
+	PpLds2& L = U.d;
+	if (tid == 0) {
+		L.tok = -1;  // "batches <= -1 done"
+		L.staged = 0;
+		L.abort_ = 0;
+		L.done[0] = L.done[1] = -1;
+	}
+	__syncthreads();
+	const int32_t len = decode_block_pp2(L, frame, frame_len, desc, b, tab_all, out);
+	if (tid == 0) {
+		if (len < 0) {
+			status[b].code = DS_RETRY;
+		} else {
+			status[b].code = DS_OK;
+			status[b].aux = 0;
+			status[b].detail = 0;
+			status[b].err_out_pos = 0;
+			status[b].out_len = uint32_t(len);
+		}
+	}
+}
+
 }  // namespace idx
 
 #ifdef LZ4ADA_IDX_STAMPS
@@ -2593,6 +3205,11 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 {
 	if (nblocks == 0)
 		return hipSuccess;
+	if (mode == 5) {  // both passes, two waves per block pipelining batches (k_decode_pp2)
+		hipLaunchKernelGGL(idx::k_decode_pp2, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
+		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
+		return hipGetLastError();
+	}
 	if (mode == 4) {  // both passes, two waves per block (k_decode_idx2)
 		hipLaunchKernelGGL(idx::k_decode_idx2, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
 		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
@@ -2615,19 +3232,20 @@ int idx_fused_mode(uint32_t nblocks)
 {
 	static const int forced = [] {
 		const char* e = getenv("LZ4ADA_IDX_WAVES");
-		return e ? (e[0] == '1' ? 3 : (e[0] == '2' ? 4 : 0)) : 0;
+		return e ? (e[0] == '1' ? 3 : (e[0] == '2' ? 4 : (e[0] == 'p' ? 5 : 0))) : 0;
 	}();
 	if (forced)
 		return forced;
 	int dev = 0, cus = 256;
 	if (hipGetDevice(&dev) == hipSuccess)
 		(void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-	return nblocks <= uint32_t(4 * cus) ? 4 : 3;
+	return nblocks <= uint32_t(4 * cus) ? 5 : 3;
 }
 
 const char* idx_fused_kernel_name(uint32_t nblocks)
 {
-	return idx_fused_mode(nblocks) == 4 ? "k_decode_idx2" : "k_decode_idx";
+	const int m = idx_fused_mode(nblocks);
+	return m == 5 ? "k_decode_pp2" : (m == 4 ? "k_decode_idx2" : "k_decode_idx");
 }
 
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
@@ -2640,8 +3258,8 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 	hipError_t err = hipMallocAsync(&tab, index_table_bytes(frame_len, nblocks), stream);
 	if (err != hipSuccess)
 		return err;
-	if (linked <= 0) {  // both passes in one launch (-1: one wave per block, -2: two)
-		const int mode = linked == -1 ? 3 : (linked == -2 ? 4 : idx_fused_mode(nblocks));
+	if (linked <= 0) {  // both passes in one launch (-1: one wave per block, -2: two, -3: pipelined pair)
+		const int mode = linked == -1 ? 3 : (linked == -2 ? 4 : (linked == -3 ? 5 : idx_fused_mode(nblocks)));
 		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
 		                            static_cast<const uint8_t*>(tab), d_out, d_status, mode, stream);
 	} else {

@@ -71,8 +71,10 @@ struct SerialState {
 enum DecVariant : int { DEC_PC = 0, DEC_IDX = 3, DEC_IDX_ALONE = 4,
                         DEC_IDX_LINKED = 5, DEC_IDX_SPARSE = 6,
                         // the fused index decoder alone with one / two waves per block
-                        DEC_IDX1_ALONE = 7, DEC_IDX2_ALONE = 8 };
-int idx_fused_mode(uint32_t nblocks);  // 3: k_decode_idx, 4: k_decode_idx2 (lz4ada_idx.hip)
+                        DEC_IDX1_ALONE = 7, DEC_IDX2_ALONE = 8,
+                        // the pipelined two-wave decoder (k_decode_pp2) alone
+                        DEC_PP2_ALONE = 9 };
+int idx_fused_mode(uint32_t nblocks);  // 3: k_decode_idx, 4: k_decode_idx2, 5: k_decode_pp2 (lz4ada_idx.hip)
 const char* idx_fused_kernel_name(uint32_t nblocks);  // the kernel idx_fused_mode picks
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,

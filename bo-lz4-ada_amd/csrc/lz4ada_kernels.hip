@@ -1401,9 +1401,9 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 	}
 	if (variant == DEC_IDX_LINKED)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream, 1);
-	if (variant == DEC_IDX1_ALONE || variant == DEC_IDX2_ALONE)
+	if (variant == DEC_IDX1_ALONE || variant == DEC_IDX2_ALONE || variant == DEC_PP2_ALONE)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream,
-		                         variant == DEC_IDX1_ALONE ? -1 : -2);
+		                         variant == DEC_IDX1_ALONE ? -1 : (variant == DEC_IDX2_ALONE ? -2 : -3));
 	if (variant == DEC_IDX || variant == DEC_IDX_ALONE || variant == DEC_IDX_SPARSE) {
 		const hipError_t err = launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out,
 		                                         d_status, stream);

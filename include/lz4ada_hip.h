@@ -253,6 +253,9 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
  * LZ4ADA_IDX_WAVES=1); declined blocks keep status code 10. */
 #define LZ4ADA_DECODE_IDX1_ALONE 7
 #define LZ4ADA_DECODE_IDX2_ALONE 8
+/* The pipelined two-wave decoder (k_decode_pp2: two waves per block taking
+ * alternate batches) alone; declined blocks keep status code 10 / 11. */
+#define LZ4ADA_DECODE_PP2_ALONE 9
 
 int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,

@@ -360,7 +360,7 @@ def _run_variant_alone(frame, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["default", "idx1", "idx2"])
+@pytest.mark.parametrize("variant", ["default", "idx1", "idx2", "pp2"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "rle", "chain"])
 @pytest.mark.parametrize("bmax", [64 << 10, 256 << 10, 4 << 20])
 def test_idx_decoder_alone(kind, bmax, variant):
@@ -376,7 +376,7 @@ def test_idx_decoder_alone(kind, bmax, variant):
         blocks.append(lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 900 + j, min(n, bmax)))
     frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, indep=True)
     v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
-         "idx2": lz4ada.DECODE_IDX2_ALONE}[variant]
+         "idx2": lz4ada.DECODE_IDX2_ALONE, "pp2": lz4ada.DECODE_PP2_ALONE}[variant]
     descs, st, out = _run_variant_alone(frame, v)
     bad = []
     for i, (c, r) in enumerate(blocks):
@@ -434,7 +434,7 @@ def oracle_blocks(frame, nblocks):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alone", ["default", "idx1", "idx2"])
+@pytest.mark.parametrize("alone", ["default", "idx1", "idx2", "pp2"])
 @pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
 def test_idx_decoder_on_vectors(name, digests, alone):
     """Reference vectors' blocks through the idx decoder (+ retry): every block
@@ -443,7 +443,7 @@ def test_idx_decoder_on_vectors(name, digests, alone):
     frame = read_vector(name, "lz4")
     info, _ = lz4ada.frame_index(frame)
     v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
-         "idx2": lz4ada.DECODE_IDX2_ALONE}[alone]
+         "idx2": lz4ada.DECODE_IDX2_ALONE, "pp2": lz4ada.DECODE_PP2_ALONE}[alone]
     descs, st, out = _run_variant_alone(frame, v)
     for i in range(info.nblocks):
         assert st[i].code in (0, lz4ada.DS_RETRY, lz4ada.DS_SPARSE), (i, st[i].code)

@@ -14,6 +14,8 @@
 #   lone     tools/lone_time.py over block sizes and classes
 #   linked   tools/linked_time.py (configs[4] phases)
 #   classes  tools/time_decode.py per content class (decoder alone and product step)
+#   pp2      the pipelined two-wave decoder: its parity tests, then timed beside
+#            k_decode_idx2 / k_decode_idx at 1,024 and 2,048 blocks
 #   gathers  tools/gathers.py (needs the LZ4ADA_IDX_GATHERS variant build)
 #
 # Every step runs under its own time limit; the first failure ends the run.
@@ -65,6 +67,14 @@ for step in "$@"; do
     for k in mixed dense literal rle; do
       timeout -k 10 200 python tools/time_decode.py --kind $k --variant idx1,product 2>&1 | grep -v amdgpu || fail classes /dev/null
     done ;;
+  pp2)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+      -k "pp2" > $O/${TAG}_pp2tests.log 2>&1 || fail pp2-tests $O/${TAG}_pp2tests.log
+    tail -2 $O/${TAG}_pp2tests.log
+    for k in mixed dense; do for nb in 1024 2048; do
+      timeout -k 10 200 python tools/time_decode.py --kind $k --blocks $nb --variant idx2,pp2,idx1 --check 2>&1 \
+        | grep -v amdgpu || fail pp2-time /dev/null
+    done; done ;;
   gathers)
     timeout -k 10 300 python tools/gathers.py --kinds mixed,dense 2>&1 | grep -v amdgpu || fail gathers /dev/null ;;
   *)
