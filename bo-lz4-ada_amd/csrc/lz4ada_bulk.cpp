@@ -388,7 +388,7 @@ int lz4ada_launch_decode_variant(const void* d_frame, uint64_t frame_len,
                                  lz4ada_block_status* d_status, int variant, void* stream)
 {
 	return guarded(nullptr, [&] {
-		if (variant < 0 || variant > 9)
+		if (variant < 0 || variant > 10)
 			raise(LZ4ADA_ASSERTION_ERROR, "unknown decoder variant");
 		HIP_OK(launch_decode_variant(static_cast<const uint8_t*>(d_frame), frame_len, d_descs,
 		                             uint32_t(nblocks), static_cast<uint8_t*>(d_out), d_status,

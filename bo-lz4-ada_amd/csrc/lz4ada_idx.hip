@@ -3258,7 +3258,8 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 	hipError_t err = hipMallocAsync(&tab, index_table_bytes(frame_len, nblocks), stream);
 	if (err != hipSuccess)
 		return err;
-	if (linked <= 0) {  // both passes in one launch (-1: one wave per block, -2: two, -3: pipelined pair)
+	const bool split = linked == -4;  // the two passes as two launches (diagnostic: per-pass counters)
+	if (linked <= 0 && !split) {  // both passes in one launch (-1: one wave per block, -2: two, -3: pipelined pair)
 		const int mode = linked == -1 ? 3 : (linked == -2 ? 4 : (linked == -3 ? 5 : idx_fused_mode(nblocks)));
 		err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
 		                            static_cast<const uint8_t*>(tab), d_out, d_status, mode, stream);
@@ -3267,7 +3268,8 @@ hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,
 		                   stream);
 		if (err == hipSuccess)
 			err = launch_decode_idx_tab(d_frame, frame_len, d_desc, nblocks,
-			                            static_cast<const uint8_t*>(tab), d_out, d_status, linked, stream);
+			                            static_cast<const uint8_t*>(tab), d_out, d_status, split ? 0 : linked,
+			                            stream);
 	}
 	const hipError_t e2 = hipFreeAsync(tab, stream);
 	return err != hipSuccess ? err : e2;

@@ -73,7 +73,9 @@ enum DecVariant : int { DEC_PC = 0, DEC_IDX = 3, DEC_IDX_ALONE = 4,
                         // the fused index decoder alone with one / two waves per block
                         DEC_IDX1_ALONE = 7, DEC_IDX2_ALONE = 8,
                         // the pipelined two-wave decoder (k_decode_pp2) alone
-                        DEC_PP2_ALONE = 9 };
+                        DEC_PP2_ALONE = 9,
+                        // k_index then k_decode_idx's pass 2, two launches (per-pass counters)
+                        DEC_IDX_SPLIT = 10 };
 int idx_fused_mode(uint32_t nblocks);  // 3: k_decode_idx, 4: k_decode_idx2, 5: k_decode_pp2 (lz4ada_idx.hip)
 const char* idx_fused_kernel_name(uint32_t nblocks);  // the kernel idx_fused_mode picks
 

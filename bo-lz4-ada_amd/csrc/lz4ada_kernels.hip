@@ -1401,6 +1401,8 @@ hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,
 	}
 	if (variant == DEC_IDX_LINKED)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream, 1);
+	if (variant == DEC_IDX_SPLIT)
+		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream, -4);
 	if (variant == DEC_IDX1_ALONE || variant == DEC_IDX2_ALONE || variant == DEC_PP2_ALONE)
 		return launch_decode_idx(d_frame, frame_len, d_desc, nblocks, d_out, d_status, stream,
 		                         variant == DEC_IDX1_ALONE ? -1 : (variant == DEC_IDX2_ALONE ? -2 : -3));

@@ -558,6 +558,7 @@ DECODE_PC, DECODE_IDX, DECODE_IDX_ALONE, DECODE_IDX_LINKED = 0, 3, 4, 5
 DECODE_IDX_SPARSE = 6
 DECODE_IDX1_ALONE, DECODE_IDX2_ALONE = 7, 8  # fused index decoder alone: one / two waves per block
 DECODE_PP2_ALONE = 9  # the pipelined two-wave decoder alone
+DECODE_IDX_SPLIT = 10  # k_index, then k_decode_idx's pass 2: two launches
 
 
 def launch_decode_variant(d_frame, frame_len, d_descs, nblocks, d_out, d_status, variant,

@@ -256,6 +256,9 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
 /* The pipelined two-wave decoder (k_decode_pp2: two waves per block taking
  * alternate batches) alone; declined blocks keep status code 10 / 11. */
 #define LZ4ADA_DECODE_PP2_ALONE 9
+/* The index decoder's two passes as two launches (k_index, then
+ * k_decode_idx's pass 2): per-pass timing and counters. */
+#define LZ4ADA_DECODE_IDX_SPLIT 10
 
 int lz4ada_launch_decode_variant(const void *d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc *d_descs, int64_t nblocks, void *d_out,

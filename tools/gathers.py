@@ -39,15 +39,16 @@ def main():
         out = torch.empty(args.blocks * bmax, dtype=torch.uint8, device=dev)
         st = torch.zeros(args.blocks * 32, dtype=torch.uint8, device=dev)
         sh = torch.cuda.current_stream(dev).cuda_stream
-        f(buf, 1)
+        f(buf, 1)  # reset (what an earlier launch left)
         lz4ada.launch_decode_variant(fr.data_ptr(), fl, de.data_ptr(), args.blocks, out.data_ptr(),
                                      st.data_ptr(), lz4ada.DECODE_IDX1_ALONE, sh)
         torch.cuda.synchronize()
+        f(buf, 1)  # this launch's counts
         loads, touches, batches, _ = list(buf)
         print(f"== {kind}: {args.blocks} blocks, {cb / 1e9:.2f} GB in, {rb / 1e9:.2f} GB out; "
               f"HBM-sourced match loads {loads / 1e6:.1f} M = {16 * loads / 1e9:.2f} GB requested, "
               f"{touches / 1e6:.1f} M line touches = {128 * touches / 1e9:.2f} GB at 128 B/line, "
-              f"{64 * touches / 1e9:.2f} GB at 64 B; {batches / args.blocks:.0f} batches per block")
+              f"{64 * touches / 1e9:.2f} GB at 64 B; {batches / args.blocks:.0f} batches per block with one")
         del fr, de, out, st
 
 
