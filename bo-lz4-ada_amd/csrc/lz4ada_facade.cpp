@@ -43,7 +43,8 @@ struct lz4ada_decompressor {
 	void hash_wait() { hasher.wait(); }
 	PinBuf stage;  // a block's output on its way to the caller's Buffer
 	PinBuf stage_hashed;  // the staging the hasher may be reading
-	PinBuf stage_st;  // its status
+	PinBuf stage_st;  // its status (the lone-block decoder writes it there itself)
+	PinBuf pin_blk;   // a lone block's compressed bytes, read by its first kernel
 	std::vector<uint8_t> blk_tmp;  // a block assembled from cached + new input
 	DevBuf<lz4ada_xxh32_state> d_tmp_hash;
 	DevBuf<SerialState> d_serial;
@@ -51,6 +52,7 @@ struct lz4ada_decompressor {
 	DevBuf<lz4ada_block_status> d_bst;
 	DevBuf<uint8_t> d_scr;  // its output, until the block checksum has passed
 	DevBuf<uint8_t> d_lone;  // the lone-block decoder's tables and words
+	bool lone_hdr_zeroed = false;  // its header (the fused chain step's count) is zero
 	hipStream_t side = nullptr;  // the block checksum, beside the fast decode
 	hipEvent_t ev_in = nullptr;
 
@@ -297,10 +299,18 @@ struct lz4ada_decompressor {
 			if (!c.first)
 				raise(LZ4ADA_CHECKSUM_ERROR, c.second);
 		}
-		if (blen > 0)
+		// a lone block goes over without a DMA copy: its first kernel reads the
+		// pinned bytes and leaves the device copy the other paths read
+		LonePlan lp;
+		const bool lone = lone_plan(blen, buflen, lp);
+		if (blen > 0 && lone) {
+			pin_blk.reserve(size_t(blen));
+			memcpy(pin_blk.p, blk, size_t(blen));
+		} else if (blen > 0) {
 			HIP_OK(hipMemcpyAsync(d_blk.p, blk, size_t(blen), hipMemcpyHostToDevice, stream));
+		}
 		phase("h2d");
-		const LoneResult lr = lone_block(blk, blen, buf, buflen, first, last);
+		const LoneResult lr = lone ? lone_block(lp, blk, blen, buf, first, last) : LONE_NOT_TAKEN;
 		phase("lone");
 		if (lr == LONE_DONE)
 			return;
@@ -468,28 +478,51 @@ struct lz4ada_decompressor {
 	// untouched for the exact path.  The status and the output come back in
 	// one round trip through pinned staging.
 	enum LoneResult { LONE_NOT_TAKEN, LONE_DONE, LONE_DECLINED };
-	LoneResult lone_block(const uint8_t* blk, int64_t blen, uint8_t* buf, int64_t buflen, int64_t& first,
-	                      int64_t& last)
+	struct LonePlan {
+		int64_t raw_len, start, cap, n0, n1;
+		bool linked;
+	};
+	// Whether the lone-block decoder takes this block, and where its output goes.
+	bool lone_plan(int64_t blen, int64_t buflen, LonePlan& p)
 	{
 		const int bcl = m.block_checksum_length;
 		const int64_t raw_len = blen - bcl;
 		if (!m.is_compressed || raw_len <= 0 || raw_len > INT32_MAX || getenv("LZ4ADA_FACADE_EXACT"))
-			return LONE_NOT_TAKEN;
+			return false;
 		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
 		const int fv = facade_variant();
 		if (!linked && !(fv < 0 && (raw_len >= LONE_MIN || fv == -2)))
-			return LONE_NOT_TAKEN;
+			return false;
 		const int64_t start = output_pos >= HISTORY_SIZE ? 0 : output_pos;  // :678-680
 		if (buflen - start <= 0)
-			return LONE_NOT_TAKEN;
+			return false;
 		int64_t cap = block_room(buflen - start, raw_len, true);
 		if (m.has_content_size)  // more output: the exact path raises mid-block, as the reference does
 			cap = int64_t(std::min<uint64_t>(uint64_t(cap), m.size_remaining));
 		if (cap <= 0 || cap > (int64_t(1) << 30))
-			return LONE_NOT_TAKEN;
-		int64_t n0 = 0, n1 = 0;
+			return false;
+		p.raw_len = raw_len;
+		p.start = start;
+		p.cap = cap;
+		p.linked = linked;
+		p.n0 = p.n1 = 0;
 		if (linked)
-			history_of(start, n0, n1);
+			history_of(start, p.n0, p.n1);
+		return true;
+	}
+
+	// The block's pinned bytes (pin_blk) through the lone-block decoder: its
+	// first kernel copies them to d_blk (for the exact path, should it
+	// decline), its last writes the output to the mirror and to the pinned
+	// staging, and the status comes back in pinned memory too -- one stream
+	// synchronisation, no DMA copy (a DMA transfer costs ~10 us of latency
+	// each way for a 64 KiB block).
+	LoneResult lone_block(const LonePlan& lp, const uint8_t* blk, int64_t blen, uint8_t* buf, int64_t& first,
+	                      int64_t& last)
+	{
+		const int bcl = m.block_checksum_length;
+		const int64_t raw_len = lp.raw_len, start = lp.start, cap = lp.cap, n0 = lp.n0, n1 = lp.n1;
+		const bool linked = lp.linked;
 		static const bool trace = getenv("LZ4ADA_TRACE_FACADE") != nullptr;
 		auto t0 = std::chrono::steady_clock::now();
 		auto lap = [&](const char* name) {
@@ -501,11 +534,20 @@ struct lz4ada_decompressor {
 			t0 = t1;
 		};
 		const int64_t sb = lone_scratch_bytes(raw_len, cap);
+		const size_t had = d_lone.n;
 		d_lone.reserve(size_t(sb));
-		HIP_OK(launch_decode_lone_parse(d_blk.p, raw_len, cap, d_bst.p, d_lone.p, sb, stream,
+		if (d_lone.n != had || !lone_hdr_zeroed) {  // a new scratch: its header zeroed once
+			HIP_OK(lone_scratch_init(d_lone.p, stream));
+			lone_hdr_zeroed = true;
+		}
+		stage.reserve(size_t(cap));
+		stage_st.reserve(sizeof(lz4ada_block_status));
+		lz4ada_block_status* hst = reinterpret_cast<lz4ada_block_status*>(stage_st.p);
+		HIP_OK(launch_decode_lone_parse(pin_blk.p, raw_len, cap, hst, d_lone.p, sb, stream,
 		                                linked ? d_buf.p + output_pos_history - n0 : nullptr, int32_t(n0),
 		                                linked ? d_buf.p : nullptr, int32_t(n1),
-		                                linked && d1_window() ? int(output_pos_history) : 0));
+		                                linked && d1_window() ? int(output_pos_history) : 0, d_blk.p, blen,
+		                                true));
 		lap("parse");
 		if (bcl > 0) {
 			const auto c = block_checksum(blk, blen);
@@ -515,28 +557,16 @@ struct lz4ada_decompressor {
 			}
 		}
 		lap("cksum");
-		HIP_OK(launch_decode_lone_emit(raw_len, d_buf.p + start, cap, d_bst.p, d_lone.p, stream,
-		                               int32_t(n0 + n1)));
-		// the likely share of the output comes back with the status
-		const int64_t spec = std::min<int64_t>(cap, std::max<int64_t>(4 * raw_len, int64_t(64) << 10));
-		stage.reserve(size_t(cap));
-		stage_st.reserve(sizeof(lz4ada_block_status));
-		HIP_OK(hipMemcpyAsync(stage_st.p, d_bst.p, sizeof(lz4ada_block_status), hipMemcpyDeviceToHost,
-		                      stream));
-		HIP_OK(hipMemcpyAsync(stage.p, d_buf.p + start, size_t(spec), hipMemcpyDeviceToHost, stream));
+		HIP_OK(launch_decode_lone_emit(raw_len, d_buf.p + start, cap, hst, d_lone.p, stream,
+		                               int32_t(n0 + n1), stage.p));
 		lap("enqueue");
 		HIP_OK(hipStreamSynchronize(stream));
 		lap("wait");
 		lz4ada_block_status st;
-		memcpy(&st, stage_st.p, sizeof st);
+		memcpy(&st, hst, sizeof st);
 		if (st.code != DS_OK)
 			return LONE_DECLINED;
 		const int64_t nout = int64_t(st.out_len);
-		if (nout > spec) {
-			HIP_OK(hipMemcpyAsync(stage.p + spec, d_buf.p + start + spec, size_t(nout - spec),
-			                      hipMemcpyDeviceToHost, stream));
-			HIP_OK(hipStreamSynchronize(stream));
-		}
 		if (m.has_content_size)
 			m.size_remaining -= uint64_t(nout);
 		output_pos = start + nout;

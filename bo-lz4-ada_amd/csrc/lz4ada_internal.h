@@ -199,12 +199,22 @@ hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, i
 // the status set to DS_RETRY on a decline) and the emit (step 4: the bytes
 // to d_out when the status is still OK).  A caller may check something on
 // the host between them, e.g. the block checksum before d_out is touched.
+// Zero-copy form (the streaming facade): d_blk may be pinned host memory
+// that step 1 reads once and copies to d_copy (ncopy >= n bytes: the
+// block's trailer too), which step 3 then reads; d_st may be pinned host
+// memory; h_out, when not null, is pinned host memory that step 4 writes
+// the bytes to as well -- no DMA copy on the block's critical path.
 hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap,
                                     lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
                                     hipStream_t stream, const uint8_t* d_h0, int32_t n0,
-                                    const uint8_t* d_h1, int32_t n1, int d1);
+                                    const uint8_t* d_h1, int32_t n1, int d1, uint8_t* d_copy = nullptr,
+                                    int64_t ncopy = 0, bool fused = false);
+// fused: a small block's chain step runs inside its windows launch, which
+// needs the scratch's header zeroed once (lone_scratch_init) before the
+// scratch's first fused use; every fused use leaves it zeroed again.
+hipError_t lone_scratch_init(void* d_scratch, hipStream_t stream);
 hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ada_block_status* d_st,
-                                   void* d_scratch, hipStream_t stream, int32_t H);
+                                   void* d_scratch, hipStream_t stream, int32_t H, uint8_t* h_out = nullptr);
 
 // host side (lz4ada_bulk.cpp): the calling thread's message for
 // lz4ada_thread_last_error() and its lz4ada_last_path() bits

@@ -223,16 +223,185 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b)
 	return (s < a || s > 0x7FFFFFFFu) ? 0x7FFFFFFFu : s;
 }
 
+// ---------------------------------------------------------------- step 2
+constexpr int32_t CT = 1024;  // k_lone_chain threads
+
+// The chain step's body for NT threads (CK windows per thread at most), E:
+// nwin + 1 entries of LDS.
+template <int32_t LW, int32_t NT, int32_t CK>
+__device__ __forceinline__ void lone_chain_body(uint32_t* E, const uint32_t* __restrict__ exit_tab,
+                                                const uint32_t* __restrict__ osum_tab,
+                                                const uint32_t* __restrict__ guess, int32_t n, int32_t nwin,
+                                                uint32_t cap, uint32_t* __restrict__ entry,
+                                                uint32_t* __restrict__ obase, LoneCtl* __restrict__ ctl,
+                                                lz4ada_block_status* __restrict__ st)
+{
+	constexpr int32_t CT = NT;
+	__shared__ uint32_t wsum[CT / 64];
+	__shared__ unsigned long long total64;
+	__shared__ int32_t first_ch;  // the first window whose successor changed this pass
+	const int32_t tid = int32_t(threadIdx.x);
+	// entry w: the first chain position >= w * LW.  Guess: the exit most
+	// positions of window w-1 reach (k_lone_windows).
+	for (int32_t w = tid; w <= nwin; w += CT)
+		E[w] = w > 0 ? guess[w] : 0u;
+	if (tid == 0)
+		total64 = 0;
+	__syncthreads();
+	// entry w+1 = the exit of entry w (or entry w itself when a sequence
+	// jumps over window w); after k passes entries 1..k are exact
+	uint32_t it = 0;
+	for (;;) {
+		++it;
+		if (tid == 0)
+			first_ch = INT32_MAX;
+		uint32_t nv[CK];
+#pragma unroll
+		for (int32_t k = 0; k < CK; ++k) {
+			const int32_t w = tid + k * CT;
+			nv[k] = 0;
+			if (w < nwin) {
+				const uint32_t e = E[w];
+				const uint32_t lim = uint32_t(min((w + 1) * LW, n));
+				nv[k] = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
+			}
+		}
+		__syncthreads();
+		int ch = 0;
+		int32_t lo = INT32_MAX;  // this thread's lowest window whose successor changed
+#pragma unroll
+		for (int32_t k = 0; k < CK; ++k) {
+			const int32_t w = tid + k * CT;
+			if (w < nwin && E[w + 1] != nv[k]) {
+				E[w + 1] = nv[k];
+				lo = min(lo, w);
+				ch = 1;
+			}
+		}
+		if (ch)
+			atomicMin(&first_ch, lo);
+		if (!__syncthreads_or(ch) || it > uint32_t(nwin) + 2)
+			break;
+		// still changing after two passes: the guesses are poor (sequences
+		// too far apart for speculative chains to merge, e.g. long literal
+		// runs).  One lane walks the first run of wrong entries, one
+		// dependent lookup per window instead of one pass per window, up to
+		// where its entry meets the stored one (the rest of that run was
+		// already right); the next pass confirms, or finds the next run
+		// (profiles/r04o_chain_walk.txt: a linked 256 KiB frame at 512-byte
+		// windows 24 -> 11 us against walking every remaining window).  The
+		// short walks are capped (ADVICE r4): from pass 2 + SHORT_WALKS on the
+		// lane walks every remaining window, so inputs with many short wrong
+		// runs cost at most a few passes more than the walk-to-the-end did.
+		constexpr uint32_t SHORT_WALKS = 3;
+		if (it >= 2) {
+			if (tid == 0) {
+				const bool to_end = it >= 2 + SHORT_WALKS;
+				for (int32_t w = first_ch; w < nwin; ++w) {
+					const uint32_t e = E[w];
+					const uint32_t lim = uint32_t(min((w + 1) * LW, n));
+					const uint32_t x = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
+					if (!to_end && w > first_ch && E[w + 1] == x)
+						break;
+					E[w + 1] = x;
+				}
+			}
+			__syncthreads();
+		}
+	}
+	// each window's output bytes along the chain; an exclusive scan places
+	// the windows (exact in 32 bits once the 64-bit total fits the slot)
+	const int32_t per = (nwin + CT - 1) / CT;
+	const int32_t w0 = tid * per;
+	uint64_t mine = 0;
+	bool bad = false;
+	uint32_t os[CK];  // the windows' output bytes, kept for the placement (per <= CK)
+#pragma unroll
+	for (int32_t k = 0; k < CK; ++k) {
+		const int32_t w = w0 + k;
+		os[k] = 0;
+		if (k < per && w < nwin) {
+			const uint32_t e = E[w];
+			if (e == NX_BAD)
+				bad = true;
+			else if (e < uint32_t(min((w + 1) * LW, n)))
+				os[k] = osum_tab[e];
+		}
+	}
+#pragma unroll
+	for (int32_t k = 0; k < CK; ++k)
+		mine += os[k];
+	if (mine)
+		atomicAdd(&total64, (unsigned long long)mine);
+	const uint32_t m32 = uint32_t(min<uint64_t>(mine, 0x3FFFFFFFull));
+	const uint32_t lane = lane_id(), wv = uint32_t(tid) >> 6;
+	const uint32_t inc = uint32_t(wave_incl_scan(int32_t(m32)));
+	if (lane == 63)
+		wsum[wv] = inc;
+	const bool anybad = __syncthreads_or(bad);
+	uint32_t run = inc - m32;
+	for (uint32_t j = 0; j < wv; ++j)
+		run += wsum[j];
+#pragma unroll
+	for (int32_t k = 0; k < CK; ++k) {
+		const int32_t w = w0 + k;
+		if (k < per && w < nwin) {
+			obase[w] = run;
+			entry[w] = E[w];
+			run += os[k];
+		}
+	}
+	if (tid == 0) {
+		const uint64_t total = total64;
+		const bool ok = !anybad && E[nwin] == uint32_t(n) && total <= uint64_t(cap);
+		ctl->code = ok ? int32_t(DS_OK) : int32_t(DS_RETRY);
+		ctl->total = ok ? uint32_t(total) : 0u;
+		ctl->nwin = uint32_t(nwin);
+		ctl->iters = it;
+		st->code = ctl->code;
+		st->out_len = ctl->total;
+	}
+}
+
+template <int32_t LW>
+__global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ exit_tab,
+                                                   const uint32_t* __restrict__ osum_tab,
+                                                   const uint32_t* __restrict__ guess,
+                                                   int32_t n, int32_t nwin, uint32_t cap,
+                                                   uint32_t* __restrict__ entry,
+                                                   uint32_t* __restrict__ obase,
+                                                   LoneCtl* __restrict__ ctl,
+                                                   lz4ada_block_status* __restrict__ st)
+{
+	extern __shared__ uint32_t E[];  // entries 0..nwin
+	lone_chain_body<LW, CT, (int32_t(16) << 20) / LW / CT>(E, exit_tab, osum_tab, guess, n, nwin, cap, entry,
+	                                                      obase, ctl, st);
+}
+
 // ---------------------------------------------------------------- step 1
 // Also the entry guess for the next window: the exit most positions of this
 // window reach (chains started at wrong bytes mostly merge into the true
 // one before the window ends), counted in an LDS hash table.
+//
+// copy (not null): blk is pinned host memory, read here once; each window
+// also writes its bytes -- the last one up to ncopy, the block's trailer --
+// to the device copy that step 3 reads.
+//
+// done (not null, zero at launch): the windows count themselves off there,
+// and the last one runs the chain step (lone_chain_body; nwin <= 2 LW, so
+// its entries fit in X) and zeroes the count again -- one launch less for
+// a small block.
 template <int32_t LW>
 __global__ __launch_bounds__(LT) void k_lone_windows(const uint8_t* __restrict__ blk, int32_t n,
                                                      uint32_t* __restrict__ exit_tab,
                                                      uint32_t* __restrict__ osum_tab,
                                                      uint32_t* __restrict__ nxt_tab,
-                                                     uint32_t* __restrict__ guess)
+                                                     uint32_t* __restrict__ guess,
+                                                     uint8_t* __restrict__ copy, int32_t ncopy,
+                                                     uint32_t* __restrict__ done, uint32_t cap,
+                                                     uint32_t* __restrict__ entry,
+                                                     uint32_t* __restrict__ obase, LoneCtl* __restrict__ ctl,
+                                                     lz4ada_block_status* __restrict__ st)
 {
 	constexpr int32_t LP = LW / LT, LSTG = 2 * LW;
 	__shared__ alignas(16) uint8_t s[LSTG + 32];
@@ -242,6 +411,11 @@ __global__ __launch_bounds__(LT) void k_lone_windows(const uint8_t* __restrict__
 	const int32_t shi = min(ws + LSTG, n);
 	cg8* in = gptr(blk);
 	lone_stage(s, in, ws, shi);
+	if (copy) {
+		const int32_t ce = blockIdx.x + 1 == gridDim.x ? ncopy : we;
+		for (int32_t i = ws + int32_t(threadIdx.x); i < ce; i += LT)
+			copy[i] = i < shi ? s[i - ws] : in[i];
+	}
 	const LoneSrc S{ s, ws, shi, in };
 	const int32_t t0 = int32_t(threadIdx.x) * LP;
 	for (int32_t k = 0; k < LP; ++k) {
@@ -338,136 +512,24 @@ __global__ __launch_bounds__(LT) void k_lone_windows(const uint8_t* __restrict__
 			}
 		guess[blockIdx.x + 1] = bc ? bk : uint32_t(min(we, n));
 	}
-}
-
-// ---------------------------------------------------------------- step 2
-constexpr int32_t CT = 1024;  // k_lone_chain threads
-
-template <int32_t LW>
-__global__ __launch_bounds__(CT) void k_lone_chain(const uint32_t* __restrict__ exit_tab,
-                                                   const uint32_t* __restrict__ osum_tab,
-                                                   const uint32_t* __restrict__ guess,
-                                                   int32_t n, int32_t nwin, uint32_t cap,
-                                                   uint32_t* __restrict__ entry,
-                                                   uint32_t* __restrict__ obase,
-                                                   LoneCtl* __restrict__ ctl,
-                                                   lz4ada_block_status* __restrict__ st)
-{
-	constexpr int32_t CK = (int32_t(16) << 20) / LW / CT;  // windows per thread (16 MiB blocks)
-	extern __shared__ uint32_t E[];  // entries 0..nwin
-	__shared__ uint32_t wsum[CT / 64];
-	__shared__ unsigned long long total64;
-	__shared__ int32_t first_ch;  // the first window whose successor changed this pass
-	const int32_t tid = int32_t(threadIdx.x);
-	// entry w: the first chain position >= w * LW.  Guess: the exit most
-	// positions of window w-1 reach (k_lone_windows).
-	for (int32_t w = tid; w <= nwin; w += CT)
-		E[w] = w > 0 ? guess[w] : 0u;
-	if (tid == 0)
-		total64 = 0;
+	if (!done)
+		return;
+	// the tables of this window out (release), counted; the last window in
+	// sees every window's (acquire) and chains them
+	__shared__ uint32_t last;
 	__syncthreads();
-	// entry w+1 = the exit of entry w (or entry w itself when a sequence
-	// jumps over window w); after k passes entries 1..k are exact
-	uint32_t it = 0;
-	for (;;) {
-		++it;
-		if (tid == 0)
-			first_ch = INT32_MAX;
-		uint32_t nv[CK];
-#pragma unroll
-		for (int32_t k = 0; k < CK; ++k) {
-			const int32_t w = tid + k * CT;
-			nv[k] = 0;
-			if (w < nwin) {
-				const uint32_t e = E[w];
-				const uint32_t lim = uint32_t(min((w + 1) * LW, n));
-				nv[k] = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
-			}
-		}
-		__syncthreads();
-		int ch = 0;
-		int32_t lo = INT32_MAX;  // this thread's lowest window whose successor changed
-#pragma unroll
-		for (int32_t k = 0; k < CK; ++k) {
-			const int32_t w = tid + k * CT;
-			if (w < nwin && E[w + 1] != nv[k]) {
-				E[w + 1] = nv[k];
-				lo = min(lo, w);
-				ch = 1;
-			}
-		}
-		if (ch)
-			atomicMin(&first_ch, lo);
-		if (!__syncthreads_or(ch) || it > uint32_t(nwin) + 2)
-			break;
-		// still changing after two passes: the guesses are poor (sequences
-		// too far apart for speculative chains to merge, e.g. long literal
-		// runs).  One lane walks the first run of wrong entries, one
-		// dependent lookup per window instead of one pass per window, up to
-		// where its entry meets the stored one (the rest of that run was
-		// already right); the next pass confirms, or finds the next run
-		// (profiles/r04o_chain_walk.txt: a linked 256 KiB frame at 512-byte
-		// windows 24 -> 11 us against walking every remaining window).  The
-		// short walks are capped (ADVICE r4): from pass 2 + SHORT_WALKS on the
-		// lane walks every remaining window, so inputs with many short wrong
-		// runs cost at most a few passes more than the walk-to-the-end did.
-		constexpr uint32_t SHORT_WALKS = 3;
-		if (it >= 2) {
-			if (tid == 0) {
-				const bool to_end = it >= 2 + SHORT_WALKS;
-				for (int32_t w = first_ch; w < nwin; ++w) {
-					const uint32_t e = E[w];
-					const uint32_t lim = uint32_t(min((w + 1) * LW, n));
-					const uint32_t x = e == NX_BAD ? NX_BAD : (e < lim ? exit_tab[e] : e);
-					if (!to_end && w > first_ch && E[w + 1] == x)
-						break;
-					E[w + 1] = x;
-				}
-			}
-			__syncthreads();
-		}
-	}
-	// each window's output bytes along the chain; an exclusive scan places
-	// the windows (exact in 32 bits once the 64-bit total fits the slot)
-	const int32_t per = (nwin + CT - 1) / CT;
-	const int32_t w0 = tid * per;
-	uint64_t mine = 0;
-	bool bad = false;
-	for (int32_t w = w0; w < min(w0 + per, nwin); ++w) {
-		const uint32_t e = E[w];
-		if (e == NX_BAD)
-			bad = true;
-		else if (e < uint32_t(min((w + 1) * LW, n)))
-			mine += osum_tab[e];
-	}
-	if (mine)
-		atomicAdd(&total64, (unsigned long long)mine);
-	const uint32_t m32 = uint32_t(min<uint64_t>(mine, 0x3FFFFFFFull));
-	const uint32_t lane = lane_id(), wv = uint32_t(tid) >> 6;
-	const uint32_t inc = uint32_t(wave_incl_scan(int32_t(m32)));
-	if (lane == 63)
-		wsum[wv] = inc;
-	const bool anybad = __syncthreads_or(bad);
-	uint32_t run = inc - m32;
-	for (uint32_t j = 0; j < wv; ++j)
-		run += wsum[j];
-	for (int32_t w = w0; w < min(w0 + per, nwin); ++w) {
-		obase[w] = run;
-		const uint32_t e = E[w];
-		entry[w] = e;
-		if (e != NX_BAD && e < uint32_t(min((w + 1) * LW, n)))
-			run += osum_tab[e];
-	}
-	if (tid == 0) {
-		const uint64_t total = total64;
-		const bool ok = !anybad && E[nwin] == uint32_t(n) && total <= uint64_t(cap);
-		ctl->code = ok ? int32_t(DS_OK) : int32_t(DS_RETRY);
-		ctl->total = ok ? uint32_t(total) : 0u;
-		ctl->nwin = uint32_t(nwin);
-		ctl->iters = it;
-		st->code = ctl->code;
-		st->out_len = ctl->total;
-	}
+	if (threadIdx.x == 0)
+		last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u ==
+		       gridDim.x;
+	__syncthreads();
+	if (!last)
+		return;
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+	if (threadIdx.x == 0)
+		__hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	const int32_t nwin = int32_t(gridDim.x);
+	lone_chain_body<LW, LT, 2 * LW / LT>(reinterpret_cast<uint32_t*>(X), exit_tab, osum_tab, guess, n, nwin,
+	                                      cap, entry, obase, ctl, st);
 }
 
 // ---------------------------------------------------------------- step 3
@@ -730,11 +792,13 @@ __device__ __forceinline__ void w_store(uint32_t* p, uint32_t v)
 
 // SL output words per workgroup: a small block takes small slices, so its
 // jump rounds spread over more CUs with fewer gathers per lane each.
+// hout (not null): pinned host memory that takes the bytes too.
 template <int32_t SL>
 __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
                                                      const LoneCtl* __restrict__ ctl,
                                                      lz4ada_block_status* __restrict__ st,
-                                                     uint8_t* __restrict__ out, uint32_t H)
+                                                     uint8_t* __restrict__ out, uint32_t H,
+                                                     uint8_t* __restrict__ hout)
 {
 	static_assert(SL % (4 * LT) == 0 && SL <= RES_SLICE, "lone-decoder tiling");
 	constexpr int32_t RPT = SL / LT;  // words per thread
@@ -794,10 +858,15 @@ __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
 			const uint32_t b = (v[4 * k] & 0xFFu) | ((v[4 * k + 1] & 0xFFu) << 8) |
 			                   ((v[4 * k + 2] & 0xFFu) << 16) | ((v[4 * k + 3] & 0xFFu) << 24);
 			*reinterpret_cast<uint32_t*>(out + i) = b;
+			if (hout)
+				*reinterpret_cast<uint32_t*>(hout + i) = b;
 		} else {
 			for (int32_t j = 0; j < 4; ++j)
-				if (i + uint32_t(j) < total)
+				if (i + uint32_t(j) < total) {
 					out[i + uint32_t(j)] = uint8_t(v[4 * k + j]);
+					if (hout)
+						hout[i + uint32_t(j)] = uint8_t(v[4 * k + j]);
+				}
 		}
 	}
 }
@@ -815,11 +884,18 @@ __global__ __launch_bounds__(LT) void k_lone_hist(uint32_t* __restrict__ W, cons
 }
 
 // ---------------------------------------------------------------- host side
+constexpr int64_t LONE_HDR = 256;  // the scratch's fixed header: the windows' done count
+
 int64_t lone_scratch_bytes(int64_t n, int64_t cap)
 {
 	const int64_t nwin = (n + LW_MIN - 1) / LW_MIN;
-	return 12 * std::max<int64_t>(n, 1) + 12 * (nwin + 2) + 64 + 4 * std::max<int64_t>(cap, 1) +
+	return LONE_HDR + 12 * std::max<int64_t>(n, 1) + 12 * (nwin + 2) + 64 + 4 * std::max<int64_t>(cap, 1) +
 	       4 * 65536 + 512;
+}
+
+hipError_t lone_scratch_init(void* d_scratch, hipStream_t stream)
+{
+	return hipMemsetAsync(d_scratch, 0, size_t(LONE_HDR), stream);
 }
 
 // Window size by compressed size n and output capacity cap, swept with
@@ -864,11 +940,12 @@ static int32_t resolve_slice(int64_t cap)
 // The scratch: per-position tables, per-window entries, the control block
 // and the words (H history words, then one per output byte).
 struct LoneLayout {
-	uint32_t *exit_tab, *osum_tab, *nxt_tab, *entry, *obase, *guess, *W;
+	uint32_t *done, *exit_tab, *osum_tab, *nxt_tab, *entry, *obase, *guess, *W;
 	LoneCtl* ctl;
 	LoneLayout(uint8_t* sc, int64_t n, int64_t nwin)
 	{
-		exit_tab = reinterpret_cast<uint32_t*>(sc);
+		done = reinterpret_cast<uint32_t*>(sc);  // first: the same place for every block size
+		exit_tab = reinterpret_cast<uint32_t*>(sc + LONE_HDR);
 		osum_tab = exit_tab + n;
 		nxt_tab = osum_tab + n;
 		entry = nxt_tab + n;
@@ -883,7 +960,8 @@ struct LoneLayout {
 template <int32_t LW>
 static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ada_block_status* d_st,
                              uint8_t* sc, hipStream_t stream, const uint8_t* d_h0, int32_t n0,
-                             const uint8_t* d_h1, int32_t n1, int d1)
+                             const uint8_t* d_h1, int32_t n1, int d1, uint8_t* d_copy, int64_t ncopy,
+                             bool fused)
 {
 	constexpr int32_t CK = (int32_t(16) << 20) / LW / CT;
 	const int64_t nwin = (n + LW - 1) / LW;
@@ -894,17 +972,25 @@ static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ad
 	uint32_t *exit_tab = Lo.exit_tab, *osum_tab = Lo.osum_tab, *nxt_tab = Lo.nxt_tab, *entry = Lo.entry,
 	         *obase = Lo.obase, *guess = Lo.guess, *W = Lo.W;
 	LoneCtl* ctl = Lo.ctl;
+	// a small block's chain step runs in its last window's workgroup
+	// (done: the count, zeroed by lone_scratch_init and again by each use)
+	uint32_t* done = fused && nwin < 2 * LW ? Lo.done : nullptr;
 	hipLaunchKernelGGL(k_lone_windows<LW>, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
-	                   exit_tab, osum_tab, nxt_tab, guess);
+	                   exit_tab, osum_tab, nxt_tab, guess, d_copy, int32_t(ncopy), done, uint32_t(cap), entry,
+	                   obase, ctl, d_st);
+	if (d_copy)
+		d_blk = d_copy;  // step 3 reads the device copy
 	hipError_t err = hipGetLastError();
 	if (err != hipSuccess)
 		return err;
-	hipLaunchKernelGGL(k_lone_chain<LW>, dim3(1), dim3(CT), size_t(nwin + 2) * 4, stream, exit_tab,
-	                   osum_tab, guess, int32_t(n), int32_t(nwin), uint32_t(cap), entry, obase, ctl,
-	                   d_st);
-	err = hipGetLastError();
-	if (err != hipSuccess)
-		return err;
+	if (!done) {
+		hipLaunchKernelGGL(k_lone_chain<LW>, dim3(1), dim3(CT), size_t(nwin + 2) * 4, stream, exit_tab,
+		                   osum_tab, guess, int32_t(n), int32_t(nwin), uint32_t(cap), entry, obase, ctl,
+		                   d_st);
+		err = hipGetLastError();
+		if (err != hipSuccess)
+			return err;
+	}
 	if (H > 0) {
 		hipLaunchKernelGGL(k_lone_hist, dim3(uint32_t((H + LT - 1) / LT)), dim3(LT), 0, stream, W, d_h0,
 		                   n0, d_h1, n1);
@@ -920,22 +1006,24 @@ static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ad
 hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap,
                                     lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,
                                     hipStream_t stream, const uint8_t* d_h0, int32_t n0,
-                                    const uint8_t* d_h1, int32_t n1, int d1)
+                                    const uint8_t* d_h1, int32_t n1, int d1, uint8_t* d_copy, int64_t ncopy,
+                                    bool fused)
 {
 	if (n <= 0 || n > (int64_t(1) << 30) || cap <= 0 || cap > (int64_t(1) << 30) ||
-	    scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 || n0 + n1 > 65535)
+	    scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 || n0 + n1 > 65535 ||
+	    (d_copy && (ncopy < n || ncopy > INT32_MAX)))
 		return hipErrorInvalidValue;
 	uint8_t* sc = static_cast<uint8_t*>(d_scratch);
 	switch (lone_window(n, cap)) {
-	case 512: return lone_steps<512>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
-	case 1024: return lone_steps<1024>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
-	case 2048: return lone_steps<2048>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
-	default: return lone_steps<4096>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1);
+	case 512: return lone_steps<512>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1, d_copy, ncopy, fused);
+	case 1024: return lone_steps<1024>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1, d_copy, ncopy, fused);
+	case 2048: return lone_steps<2048>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1, d_copy, ncopy, fused);
+	default: return lone_steps<4096>(d_blk, n, cap, d_st, sc, stream, d_h0, n0, d_h1, n1, d1, d_copy, ncopy, fused);
 	}
 }
 
 hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ada_block_status* d_st,
-                                   void* d_scratch, hipStream_t stream, int32_t H)
+                                   void* d_scratch, hipStream_t stream, int32_t H, uint8_t* h_out)
 {
 	const int32_t lw = lone_window(n, cap);
 	const int64_t nwin = (n + lw - 1) / lw;
@@ -945,15 +1033,15 @@ hipError_t launch_decode_lone_emit(int64_t n, uint8_t* d_out, int64_t cap, lz4ad
 	switch (sl) {
 	case 1024:
 		hipLaunchKernelGGL(k_lone_resolve<1024>, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st, d_out,
-		                   uint32_t(H));
+		                   uint32_t(H), h_out);
 		break;
 	case 2048:
 		hipLaunchKernelGGL(k_lone_resolve<2048>, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st, d_out,
-		                   uint32_t(H));
+		                   uint32_t(H), h_out);
 		break;
 	default:
 		hipLaunchKernelGGL(k_lone_resolve<RES_SLICE>, dim3(nres), dim3(LT), 0, stream, Lo.W, Lo.ctl, d_st,
-		                   d_out, uint32_t(H));
+		                   d_out, uint32_t(H), h_out);
 	}
 	return hipGetLastError();
 }
