@@ -93,8 +93,10 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		HIP_OK(hipMemcpyAsync(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc),
 		                      hipMemcpyHostToDevice, stream));
 		HIP_OK(hipMemsetAsync(sx.p, 0, sb, stream));
+		// the checksums ride beside the index and decodes (side stream),
+		// joined before the statuses are read
+		HIP_OK(launch_block_checksums_beside(d_frame, d_desc.p, nb, sx.p, stream));
 		HIP_OK(launch_link_fill(bx.p, by.p, bh.p, d_desc.p, nb, stream));
-		HIP_OK(launch_block_checksums(d_frame, d_desc.p, nb, sx.p, stream));
 		HIP_OK(launch_index(d_frame, frame_len, d_desc.p, nb, tab.p, sx.p, stream));
 		HIP_OK(hipMemcpyAsync(sy.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
 		HIP_OK(hipMemcpyAsync(sh.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
@@ -106,6 +108,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bufs[k], sts[k], 1, LINK_HIST,
 			                        stream));
 		}
+		HIP_OK(join_block_checksums(stream));
 		phase("decodes");
 		std::vector<lz4ada_block_status> st(nb);
 		d2h(st.data(), sx.p, sb, stream);
@@ -161,7 +164,6 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		d_A.reserve(nb);
 		d_ctr.reserve(2);
 		HIP_OK(hipMemcpyAsync(d_A.p, A.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
-		HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
 		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
 		uint32_t ctr[2] = { 0, 0 };
 		uint8_t* F = nullptr;
@@ -187,9 +189,12 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			// first round reads only those
 			HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
 			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
-			                        act + ns, d_ctr.p, stream));
-			d2h(ctr, d_ctr.p, sizeof ctr, stream);
+			                        act + ns, stream));
 			phase("init");
+			// the first round always runs: init's span flags leave it nothing
+			// to read when no byte came from history (a count would cost an
+			// atomic per wave and a round trip)
+			ctr[0] = 1;
 			for (int round = 0; ctr[0] > 0; ++round) {
 				if (round > 64)
 					return BULK_EXACT;  // never expected: every pointer goes strictly back

@@ -166,10 +166,17 @@ hipError_t launch_serial_block(uint8_t* d_buf, int64_t buflen, const uint8_t* d_
 // three decode buffers are preceded by 64 KiB history regions.
 hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_block_desc* d_desc,
                             uint32_t nblocks, hipStream_t stream);
+// The block checksums on this thread's side stream, forked from stream
+// (they write only the statuses' cksum fields, so kernels on stream may
+// fill the other fields meanwhile); join_block_checksums makes stream wait
+// for them.
+hipError_t launch_block_checksums_beside(const uint8_t* d_frame, const lz4ada_block_desc* d_desc,
+                                        uint32_t nblocks, lz4ada_block_status* d_status, hipStream_t stream);
+hipError_t join_block_checksums(hipStream_t stream);
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
                             const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
                             const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                            uint8_t* d_F, uint8_t* d_act, uint32_t* d_ctr, hipStream_t stream);
+                            uint8_t* d_F, uint8_t* d_act, hipStream_t stream);
 // One pointer-jumping round; d_act_in (nullptr: every span) / d_act_out:
 // a byte per span of positions, 1 while the span holds an unresolved word.
 int64_t link_spans(int64_t n);

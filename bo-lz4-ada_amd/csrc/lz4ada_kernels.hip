@@ -1501,6 +1501,29 @@ static hipError_t side_stream(SideStream*& out)
 	return hipSuccess;
 }
 
+hipError_t launch_block_checksums_beside(const uint8_t* d_frame, const lz4ada_block_desc* d_desc,
+                                        uint32_t nblocks, lz4ada_block_status* d_status, hipStream_t stream)
+{
+	SideStream* side = nullptr;
+	hipError_t err = side_stream(side);
+	if (err == hipSuccess)
+		err = hipEventRecord(side->fork, stream);
+	if (err == hipSuccess)
+		err = hipStreamWaitEvent(side->s, side->fork, 0);
+	if (err == hipSuccess)
+		err = launch_block_checksums(d_frame, d_desc, nblocks, d_status, side->s);
+	if (err == hipSuccess)
+		err = hipEventRecord(side->join, side->s);
+	return err;
+}
+
+hipError_t join_block_checksums(hipStream_t stream)
+{
+	SideStream* side = nullptr;
+	const hipError_t err = side_stream(side);
+	return err != hipSuccess ? err : hipStreamWaitEvent(stream, side->join, 0);
+}
+
 hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,
                                  const lz4ada_block_desc* d_desc, uint32_t nblocks,
                                  uint8_t* d_out, lz4ada_block_status* d_status,
