@@ -191,6 +191,17 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
 			                        act + ns, stream));
 			phase("init");
+			auto spans_flagged = [&](const uint8_t* a) {  // (trace only) spans a round will visit
+				if (!trace)
+					return;
+				std::vector<uint8_t> h(static_cast<size_t>(ns));
+				d2h(h.data(), a, size_t(ns), stream);
+				size_t c = 0;
+				for (uint8_t v : h)
+					c += v != 0;
+				fprintf(stderr, "[linked] spans     %zu of %lld flagged\n", c, (long long)ns);
+			};
+			spans_flagged(act + ns);
 			// the first round always runs: init's span flags leave it nothing
 			// to read when no byte came from history (a count would cost an
 			// atomic per wave and a round trip)
@@ -204,6 +215,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out, d_ctr.p,
 				                        stream));
 				d2h(ctr, d_ctr.p, sizeof ctr, stream);
+				spans_flagged(a_out);
 				if (ctr[1])
 					return BULK_EXACT;  // a reference before the frame start: the exact error
 			}
