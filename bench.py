@@ -179,7 +179,7 @@ def make_unique_blocks(lz4ada, lz4frame, xxhash, kind, n_unique, block_max, bloc
     return recs
 
 
-def assemble_shard(lz4ada, torch, recs, first_block, nblocks, block_max, dev):
+def assemble_shard(lz4ada, torch, recs, first_block, nblocks, block_max, dev, slot_pad=0):
     """This rank's shard of the tiled frame: the unique blocks cycle with
     period len(recs) from `first_block`, so one period (rotated to start
     there) is assembled in host memory, copied to the GPU once and tiled on
@@ -220,7 +220,7 @@ def assemble_shard(lz4ada, torch, recs, first_block, nblocks, block_max, dev):
         stored = (int.from_bytes(rec[:4], "little") >> 31) & 1
         has_ck = len(rec) == clen + 8
         d.flags = (lz4ada.BLOCK_STORED if stored else 0) | (lz4ada.BLOCK_HAS_CKSUM if has_ck else 0)
-        d.out_off = i * block_max
+        d.out_off = i * (block_max + slot_pad)  # slot_pad: layout experiments only
         d.out_cap = block_max
         d.cksum = int.from_bytes(rec[4 + clen:8 + clen], "little") if has_ck else 0
         exp_hash.append(h)

@@ -31,9 +31,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kinds", default="mixed")
     ap.add_argument("--blocks", type=int, default=2048)
+    ap.add_argument("--block-max", type=int, default=4 << 20)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    bmax = 4 << 20
+    bmax = args.block_max
     f = lz4ada._lib.lz4ada_idx_stamps
     f.argtypes = [ctypes.c_void_p, ctypes.c_int]
     buf = (ctypes.c_ulonglong * len(NAMES))()

@@ -38,15 +38,17 @@ def main():
     ap.add_argument("--variant", default="idx", help=",".join(VARIANTS) + ",product")
     ap.add_argument("--no-bcksum", action="store_true")
     ap.add_argument("--check", action="store_true", help="golden-check the output once")
+    ap.add_argument("--block-max", type=int, default=4 << 20)
+    ap.add_argument("--slot-pad", type=int, default=0, help="bytes between output slots (layout experiment)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    bmax = 4 << 20
+    bmax = args.block_max
     M = (lz4ada, lz4frame, xxhash, torch)
     recs = bench.make_unique_blocks(lz4ada, lz4frame, xxhash, args.kind, args.unique, bmax,
                                     block_cksum=not args.no_bcksum)
     d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = bench.assemble_shard(
-        lz4ada, torch, recs, 0, args.blocks, bmax, dev)
-    d_out = torch.empty(args.blocks * bmax, dtype=torch.uint8, device=dev)
+        lz4ada, torch, recs, 0, args.blocks, bmax, dev, slot_pad=args.slot_pad)
+    d_out = torch.empty(args.blocks * (bmax + args.slot_pad), dtype=torch.uint8, device=dev)
     d_status = torch.zeros(args.blocks * 32, dtype=torch.uint8, device=dev)
     sh = torch.cuda.current_stream(dev).cuda_stream
     d_hash = torch.zeros(args.blocks, dtype=torch.int32, device=dev)
