@@ -70,11 +70,13 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			x.out_off = bytes + uint64_t(HISTORY_SIZE);
 			bytes += uint64_t(HISTORY_SIZE) + round256(x.out_cap);
 		}
+		// two planes for every block (x: history k -> k & 255; z: literals
+		// as zeros, history k -> k >> 8), two more (y, h) only for the blocks
+		// z cannot serve
 		struct {
 			uint8_t* p;
-		} bx{ scratch(SC_X, size_t(bytes)) }, by{ bx.p ? scratch(SC_Y, size_t(bytes)) : nullptr },
-		    bh{ by.p ? scratch(SC_H, size_t(bytes)) : nullptr },
-		    tab{ bh.p ? scratch(SC_TAB, index_table_bytes(frame_len, nb)) : nullptr };
+		} bx{ scratch(SC_X, size_t(bytes)) }, bz{ bx.p ? scratch(SC_Z, size_t(bytes)) : nullptr },
+		    tab{ bz.p ? scratch(SC_TAB, index_table_bytes(frame_len, nb)) : nullptr };
 		if (!tab.p) {
 			if (budget > (uint64_t(64) << 20) && nb > 1) {
 				budget /= 2;
@@ -83,11 +85,10 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			return BULK_EXACT;
 		}
 		DevBuf<lz4ada_block_desc> d_desc;
-		DevBuf<lz4ada_block_status> sx, sy, sh;
+		DevBuf<lz4ada_block_status> sx, sz;
 		d_desc.reserve(nb);
 		sx.reserve(nb);
-		sy.reserve(nb);
-		sh.reserve(nb);
+		sz.reserve(nb);
 		const size_t sb = nb * sizeof(lz4ada_block_status);
 		phase("alloc");
 		HIP_OK(hipMemcpyAsync(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc),
@@ -96,21 +97,16 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		// the checksums ride beside the index and decodes (side stream),
 		// joined before the statuses are read
 		HIP_OK(launch_block_checksums_beside(d_frame, d_desc.p, nb, sx.p, stream));
-		HIP_OK(launch_link_fill(bx.p, by.p, bh.p, d_desc.p, nb, stream));
+		HIP_OK(launch_link_fill(bx.p, nullptr, bz.p, d_desc.p, nb, stream));
 		HIP_OK(launch_index(d_frame, frame_len, d_desc.p, nb, tab.p, sx.p, stream));
-		HIP_OK(hipMemcpyAsync(sy.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
-		HIP_OK(hipMemcpyAsync(sh.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
-		uint8_t* bufs[3] = { bx.p, by.p, bh.p };
-		lz4ada_block_status* sts[3] = { sx.p, sy.p, sh.p };
-		for (int k = 0; k < 3; ++k) {
-			HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bufs[k], sts[k], 2,
-			                             stream));
-			HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bufs[k], sts[k], 1, LINK_HIST,
-			                        stream));
-		}
+		HIP_OK(hipMemcpyAsync(sz.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
+		HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bx.p, sx.p, 2, stream));
+		HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bx.p, sx.p, 1, LINK_HIST, stream));
+		HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bz.p, sz.p, 6, stream));
 		HIP_OK(join_block_checksums(stream));
 		phase("decodes");
-		std::vector<lz4ada_block_status> st(nb);
+		std::vector<lz4ada_block_status> st(nb), stz(nb);
+		HIP_OK(hipMemcpyAsync(stz.data(), sz.p, sb, hipMemcpyDeviceToHost, stream));
 		d2h(st.data(), sx.p, sb, stream);
 		std::vector<int64_t> A(nb);
 		int64_t n = 0;
@@ -154,6 +150,53 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			}
 			return BULK_EXACT;
 		}
+		// blocks plane z cannot serve alone: one that reads history positions
+		// below 256 (AUX_DEEP_HIST: their high byte is 0, like a literal's)
+		// takes plane y too (x != y marks a history byte, k = x | z << 8);
+		// one z's decoder declined (oversized batches, anything pass 1
+		// declined) takes y and h -- the three-plane rule.  Every other block
+		// is DS_SKIP in those launches.
+		std::vector<uint8_t> mode(nb, 0);
+		uint32_t ny = 0, nh = 0;
+		for (uint32_t i = 0; i < nb; ++i) {
+			if (stz[i].code != DS_OK)
+				mode[i] = 2;
+			else if (stz[i].aux & AUX_DEEP_HIST)
+				mode[i] = 1;
+			ny += mode[i] != 0;
+			nh += mode[i] == 2;
+		}
+		uint8_t *py = nullptr, *ph = nullptr;
+		DevBuf<uint8_t> d_mode;
+		if (ny) {
+			py = scratch(SC_Y, size_t(bytes));
+			ph = py && nh ? scratch(SC_H, size_t(bytes)) : nullptr;
+			if (!py || (nh && !ph))
+				return BULK_EXACT;
+			d_mode.reserve(nb);
+			HIP_OK(hipMemcpyAsync(d_mode.p, mode.data(), nb, hipMemcpyHostToDevice, stream));
+			HIP_OK(launch_link_fill(nullptr, py, ph, d_desc.p, nb, stream));
+			std::vector<lz4ada_block_status> s_plane[2];
+			for (int k = 0; k < (nh ? 2 : 1); ++k) {
+				std::vector<lz4ada_block_status> s3(stz);
+				for (uint32_t i = 0; i < nb; ++i)
+					if (mode[i] <= k)  // y: modes 1 and 2; h: mode 2
+						s3[i].code = DS_SKIP;
+				DevBuf<lz4ada_block_status> s_dev;
+				s_dev.reserve(nb);
+				HIP_OK(hipMemcpyAsync(s_dev.p, s3.data(), sb, hipMemcpyHostToDevice, stream));
+				uint8_t* buf = k == 0 ? py : ph;
+				HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, buf, s_dev.p, 2, stream));
+				HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, buf, s_dev.p, 1, LINK_HIST, stream));
+				s_plane[k].resize(nb);
+				d2h(s_plane[k].data(), s_dev.p, sb, stream);
+				for (uint32_t i = 0; i < nb; ++i)
+					if (mode[i] > k &&
+					    (s_plane[k][i].code != DS_OK || s_plane[k][i].out_len != st[i].out_len))
+						return BULK_EXACT;  // never expected: plane x decoded it
+			}
+			phase("more planes");
+		}
 		DevBuf<int64_t> d_A;
 		DevBuf<uint32_t> d_ctr;
 		struct {
@@ -188,8 +231,8 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			// init flags the spans that hold a history-derived byte: the
 			// first round reads only those
 			HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
-			HIP_OK(launch_link_init(bx.p, by.p, bh.p, d_desc.p, sx.p, d_A.p, nb, block_max, d_P.p, F,
-			                        act + ns, stream));
+			HIP_OK(launch_link_init(bx.p, bz.p, py, ph, ny ? d_mode.p : nullptr, d_desc.p, sx.p, d_A.p, nb,
+			                        block_max, d_P.p, F, act + ns, stream));
 			phase("init");
 			auto spans_flagged = [&](const uint8_t* a) {  // (trace only) spans a round will visit
 				if (!trace)

@@ -132,6 +132,16 @@ __device__ unsigned long long g_idx_gathers[4];  // loads, line touches, batches
 #define GCOUNT(i, v)
 #endif
 
+// 16 bytes of global memory at p (any alignment): a non-template home for
+// the memcpy (clang rejects __builtin_memcpy on a global-address-space
+// pointer inside a device function template)
+__device__ __forceinline__ u32x4 ldg16(const GLOBAL uint8_t* p)
+{
+	u32x4 v;
+	__builtin_memcpy(&v, p, 16);
+	return v;
+}
+
 // ---------------------------------------------------------------- byte access
 // Block-relative byte p comes from LDS when [p, p+8) lies in the staged
 // window [lo, hi), else from global memory (guarded by the frame end).
@@ -1326,6 +1336,16 @@ __device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_
 // matches may read -- 0 for independent blocks; in a linked frame, the
 // earlier blocks' output, contiguous when every one of them is full.
 // Returns the block's status code; out_len gets its output length.
+//
+// ZL (the linked path's second plane, k_decode_idx_zl): every literal byte
+// is written as 0, so an output byte is nonzero only where it came from
+// the synthetic history (whose bytes there hold the history position's
+// high byte); a match reading history positions below 256 (more than
+// 65,280 bytes before the block: their high byte is 0 too) sets
+// AUX_DEEP_HIST; a stored block is all zeros; an oversized batch (literals
+// straight to HBM) declines the block, which then takes the three-plane
+// decode (lz4ada_bulk_linked.cpp).
+template <bool ZL = false>
 __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __restrict__ frame,
                                                 uint64_t frame_len,
                                                 const lz4ada_block_desc* __restrict__ desc,
@@ -1350,6 +1370,9 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		int32_t code = DS_OK;
 		if (n > cap) {
 			code = DS_OUT_OVERFLOW;
+		} else if (ZL) {  // every byte a literal: zeros
+			for (int32_t x = 16 * lane; x < n; x += 64 * 16)
+				gstore_n(ob + x, u32x4{ 0u, 0u, 0u, 0u }, min(16, n - x));
 		} else {
 			Src S0;
 			S0.in = in;
@@ -1413,6 +1436,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 	int32_t o_batch = 0;  // output position of the current batch
 	bool bad = false;
 	bool d1 = false;  // a match with offset >= D1_OFF reads before the block start
+	bool deep = false;  // ZL: a match reads history positions below 256
 	for (int32_t k0 = 0; k0 < nsub && !bad;) {
 		// stage input so that [k0*SUB, k0*SUB + 4 KiB) is readable
 		const int32_t cf = (k0 * SUB + mis) / BATCH;
@@ -1460,6 +1484,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		ISTAMP(D_WALK1);
 
 		if (m == 0) {
+			if (ZL) {  // (literals straight to HBM: the three-plane decode takes the block)
+				bad = true;
+				break;
+			}
 			// oversized: all 64 sub-segments straight to HBM
 			const int32_t total = __shfl(incl, 63);
 			if (o_batch + total > cap) {
@@ -1537,6 +1565,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 							pre = true;  // reference before the block start (D2) / history
 						if (roff[r] > mdst && roff[r] >= D1_OFF)
 							d1 = true;
+						if (ZL && roff[r] > mdst + 65280)
+							deep = true;
 						if (mdst - roff[r] < glo)
 							anyg = true;
 					}
@@ -1582,7 +1612,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #ifdef LZ4ADA_IDX_EXP_NOVG  // timing experiment: no HBM match loads (wrong output)
 							vg[r][c] = u32x4{uint32_t(src), 0u, 0u, 0u};
 #else
-							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
+							vg[r][c] = ldg16(ob + src + 16 * c);
 #endif
 					nc[r] = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
 					GCOUNT(0, __popcll(__ballot(g)));
@@ -1620,7 +1650,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #ifdef LZ4ADA_IDX_EXP_NOVG
 					vr = u32x4{uint32_t(od - ooff), 0u, 0u, 0u};
 #else
-					__builtin_memcpy(&vr, ob + (od - ooff) + 16 * k, 16);
+					vr = ldg16(ob + (od - ooff) + 16 * k);
 #endif
 				}
 				wave_lds_fence();  // ldesc / own[] are written again later
@@ -1640,7 +1670,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r)
 				if (rL[r] > 0)  // rL = 0 also where a round has no sequence
-					ostore(D, rdst[r], fetch16(S, rlit[r]), min(16, rL[r]));
+					ostore(D, rdst[r], ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, rlit[r]), min(16, rL[r]));
 			const int32_t nc0 = rL[0] > 16 ? (rL[0] - 1) >> 4 : 0;
 			const int32_t nc1 = rL[1] > 16 ? (rL[1] - 1) >> 4 : 0;
 			if (__any(nc0 > 0 || nc1 > 0)) {
@@ -1663,7 +1693,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					const int32_t L = int32_t((dd >> 32) & 0xffffu);
 					const int32_t k = 1 + t - int32_t(dd >> 48);  // piece 0 went in-lane
 					if (t < tot)
-						ostore(D, dst + 16 * k, fetch16(S, lit + 16 * k), min(16, L - 16 * k));
+						ostore(D, dst + 16 * k, ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, lit + 16 * k),
+						       min(16, L - 16 * k));
 				}
 			}
 		}
@@ -1719,7 +1750,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 						const int32_t oml = __shfl(ml, lo);
 						if (t < rtot[r]) {
 							u32x4 v;
-							__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
+							v = ldg16(ob + osrc + 16 * k);
 							ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
 						}
 					}
@@ -1779,6 +1810,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		ISTAMP(D_FLUSH);
 	}
 	d1 = __any(d1);
+	deep = __any(deep);
 	if (!bad && lane == 0 && (o_batch & 15))  // last partial unit
 		gstore_n(ob + (o_batch & ~15), *reinterpret_cast<const u32x4*>(&D.oring[(o_batch & ~15) & OMASK]),
 		         o_batch & 15);
@@ -1787,7 +1819,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			status[b].code = DS_RETRY;
 		} else {
 			status[b].code = DS_OK;
-			status[b].aux = d1 ? AUX_D1_RISK : 0;
+			status[b].aux = (d1 ? AUX_D1_RISK : 0) | (deep ? AUX_DEEP_HIST : 0);
 			status[b].detail = 0;
 			status[b].err_out_pos = 0;
 			status[b].out_len = uint32_t(o_batch);
@@ -1861,6 +1893,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 			status[r].code = DS_RETRY;
 }
 
+
+// The linked path's literal-zero plane (decode_block<true>): pass 2 of every
+// block in the history layout, one wave per block.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_idx_zl(
+        const uint8_t* __restrict__ frame, uint64_t frame_len, const lz4ada_block_desc* __restrict__ desc,
+        uint32_t nblocks, uint8_t* __restrict__ tab_all, uint8_t* __restrict__ out,
+        lz4ada_block_status* __restrict__ status)
+{
+	__shared__ DecLds D;
+	if (blockIdx.x >= nblocks)
+		return;
+	int32_t len;
+	decode_block<true>(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, LINK_HIST, len);
+}
 
 // ============================================================ two waves
 // k_decode_idx2: the fused decode of k_decode_idx with TWO waves per block
@@ -3205,6 +3251,11 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 {
 	if (nblocks == 0)
 		return hipSuccess;
+	if (mode == 6) {  // pass 2, linked layout, literals as zeros (k_decode_idx_zl)
+		hipLaunchKernelGGL(idx::k_decode_idx_zl, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
+		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
+		return hipGetLastError();
+	}
 	if (mode == 5) {  // both passes, two waves per block pipelining batches (k_decode_pp2)
 		hipLaunchKernelGGL(idx::k_decode_pp2, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
 		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);

@@ -32,6 +32,9 @@ constexpr int32_t LINK_HIST = 65535;
 // DS_OK block) and the host sends those frames to the exact path.
 constexpr int32_t D1_OFF = int32_t(HISTORY_SIZE) - 7;
 constexpr int32_t AUX_D1_RISK = 1;
+// the linked path's literal-zero decode (k_decode_idx_zl): a match reads
+// history positions below 256, whose high byte is 0 like a literal's
+constexpr int32_t AUX_DEEP_HIST = 2;
 
 // Device status codes written by the decode kernels (per block).
 enum DevStatus : int32_t {
@@ -48,6 +51,7 @@ enum DevStatus : int32_t {
 	DS_RETRY = 10,         // a fast decoder declined the block: k_decode_pc (or the exact path) redoes it
 	DS_SPARSE = 11,        // pass 1 declined a literal-heavy block: k_decode_sparse takes it
 	                       // (k_decode_pc, retry_only, takes it like DS_RETRY)
+	DS_SKIP = 12,          // not part of this launch: every decoder leaves the block alone
 };
 
 // State of the serial reference-exact block kernel (emulates one
@@ -173,10 +177,14 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 hipError_t launch_block_checksums_beside(const uint8_t* d_frame, const lz4ada_block_desc* d_desc,
                                         uint32_t nblocks, lz4ada_block_status* d_status, hipStream_t stream);
 hipError_t join_block_checksums(hipStream_t stream);
-hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
-                            const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
-                            const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                            uint8_t* d_F, uint8_t* d_act, hipStream_t stream);
+// Words from the planes: x (history k -> k & 255) and z (literals 0,
+// history k -> k >> 8) for every block; d_three (nullable) gives a block's
+// mode -- 1: y (~x) as well, 2: x, y and h (k >> 8) instead.
+hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y, const uint8_t* h,
+                            const uint8_t* d_three, const lz4ada_block_desc* d_desc,
+                            const lz4ada_block_status* d_st, const int64_t* d_A, uint32_t nblocks,
+                            int64_t block_max, uint32_t* d_P, uint8_t* d_F, uint8_t* d_act,
+                            hipStream_t stream);
 // One pointer-jumping round; d_act_in (nullptr: every span) / d_act_out:
 // a byte per span of positions, 1 while the span holds an unresolved word.
 int64_t link_spans(int64_t n);

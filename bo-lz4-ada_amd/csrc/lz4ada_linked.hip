@@ -56,7 +56,9 @@ __device__ __forceinline__ void flag_any(uint32_t* flag, bool v)
 		__hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// History regions of the three decode buffers.
+// History regions of the decode buffers (a null plane is skipped): x = k &
+// 255, y = ~x, h = k >> 8 at region byte k (the literal-zero plane z takes
+// h's pattern).
 __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint8_t* __restrict__ y,
                                                    uint8_t* __restrict__ h,
                                                    const lz4ada_block_desc* __restrict__ desc,
@@ -77,9 +79,12 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 		}
 		vx = u32x4{ w[0], w[1], w[2], w[3] };
 		const uint32_t hi = (k0 >> 8) * 0x01010101u;
-		*reinterpret_cast<GLOBAL u32x4*>(gptr(x) + base + k0) = vx;
-		*reinterpret_cast<GLOBAL u32x4*>(gptr(y) + base + k0) = ~vx;
-		*reinterpret_cast<GLOBAL u32x4*>(gptr(h) + base + k0) = u32x4{ hi, hi, hi, hi };
+		if (x)
+			*reinterpret_cast<GLOBAL u32x4*>(gptr(x) + base + k0) = vx;
+		if (y)
+			*reinterpret_cast<GLOBAL u32x4*>(gptr(y) + base + k0) = ~vx;
+		if (h)
+			*reinterpret_cast<GLOBAL u32x4*>(gptr(h) + base + k0) = u32x4{ hi, hi, hi, hi };
 	}
 }
 
@@ -92,8 +97,10 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
 
 __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x,
-                                                   const uint8_t* __restrict__ y,
-                                                   const uint8_t* __restrict__ h,
+                                                   const uint8_t* __restrict__ z,
+                                                   const uint8_t* __restrict__ y3,
+                                                   const uint8_t* __restrict__ h3,
+                                                   const uint8_t* __restrict__ three,
                                                    const lz4ada_block_desc* __restrict__ desc,
                                                    const lz4ada_block_status* __restrict__ st,
                                                    const int64_t* __restrict__ A, uint32_t nblocks,
@@ -111,6 +118,14 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 	const int32_t lane = int32_t(lane_id());
 	const bool aligned = (ab & 3) == 0;
 	const uint32_t hb = uint32_t(ab);  // + k: history position k's source, encoded + 65536
+	// mode 0, planes x and z: a byte came from history iff z != 0, k = x |
+	// z << 8; mode 1 (history positions below 256 read), x, z and y: iff z
+	// != 0 or x != y, k = x | z << 8; mode 2 (z not decoded), x, y and h:
+	// iff x != y, k = x | h << 8
+	const uint32_t md = three ? three[b] : 0u;
+	const bool tri = md != 0;
+	const uint8_t* __restrict__ y = tri ? y3 : z;
+	const uint8_t* __restrict__ h = md == 2 ? h3 : z;
 	// a wave takes 1 KiB of the block at a time, lane l its bytes g0 + 4 l +
 	// 256 j (j < 4): every load (a dword of each copy), word store (16 bytes)
 	// and byte store (a dword) of the wave is one contiguous run (round 4
@@ -125,13 +140,14 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 			wx[j] = wy[j] = wh[j] = 0;
 			if (q + 4 <= len) {
 				wx[j] = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(x) + ob + q);
-				wy[j] = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(y) + ob + q);
+				if (tri)
+					wy[j] = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(y) + ob + q);
 				wh[j] = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(h) + ob + q);
 			} else {
 				for (int i = 0; i < 4; ++i)
 					if (q + i < len) {
 						wx[j] |= uint32_t(x[ob + q + i]) << (8 * i);
-						wy[j] |= uint32_t(y[ob + q + i]) << (8 * i);
+						wy[j] |= tri ? uint32_t(y[ob + q + i]) << (8 * i) : 0u;
 						wh[j] |= uint32_t(h[ob + q + i]) << (8 * i);
 					}
 			}
@@ -151,7 +167,8 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 				const uint32_t bx = (wx[j] >> (8 * i)) & 255u;
 				const uint32_t by = (wy[j] >> (8 * i)) & 255u;
 				const uint32_t bh = (wh[j] >> (8 * i)) & 255u;
-				const uint32_t hist = (bx != by && i < nv) ? 0xFFFFFFFFu : 0u;
+				const bool from_hist = md == 2 ? bx != by : (bh != 0u || (md == 1 && bx != by));
+				const uint32_t hist = (from_hist && i < nv) ? 0xFFFFFFFFu : 0u;
 				const uint32_t lit = RES | bx, ptr = hb + (bx | (bh << 8));
 				v[i] = lit ^ ((lit ^ ptr) & hist);
 				u += hist & 1u;
@@ -322,10 +339,11 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 	return hipGetLastError();
 }
 
-hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h,
-                            const lz4ada_block_desc* d_desc, const lz4ada_block_status* d_st,
-                            const int64_t* d_A, uint32_t nblocks, int64_t block_max, uint32_t* d_P,
-                            uint8_t* d_F, uint8_t* d_act, hipStream_t stream)
+hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y, const uint8_t* h,
+                            const uint8_t* d_three, const lz4ada_block_desc* d_desc,
+                            const lz4ada_block_status* d_st, const int64_t* d_A, uint32_t nblocks,
+                            int64_t block_max, uint32_t* d_P, uint8_t* d_F, uint8_t* d_act,
+                            hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
@@ -333,8 +351,8 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* y, const uint8_t* h
 	// million 1 KiB workgroups cost more in dispatch than in work
 	const int64_t per = 4 * 16 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
-	hipLaunchKernelGGL(link::k_link_init, dim3(gy, nblocks), dim3(link::TPB), 0, stream, x, y, h, d_desc,
-	                   d_st, d_A, nblocks, d_P, d_F, d_act);
+	hipLaunchKernelGGL(link::k_link_init, dim3(gy, nblocks), dim3(link::TPB), 0, stream, x, z, y, h, d_three,
+	                   d_desc, d_st, d_A, nblocks, d_P, d_F, d_act);
 	return hipGetLastError();
 }
 
