@@ -132,16 +132,6 @@ __device__ unsigned long long g_idx_gathers[4];  // loads, line touches, batches
 #define GCOUNT(i, v)
 #endif
 
-// 16 bytes of global memory at p (any alignment): a non-template home for
-// the memcpy (clang rejects __builtin_memcpy on a global-address-space
-// pointer inside a device function template)
-__device__ __forceinline__ u32x4 ldg16(const GLOBAL uint8_t* p)
-{
-	u32x4 v;
-	__builtin_memcpy(&v, p, 16);
-	return v;
-}
-
 // ---------------------------------------------------------------- byte access
 // Block-relative byte p comes from LDS when [p, p+8) lies in the staged
 // window [lo, hi), else from global memory (guarded by the frame end).
@@ -1337,7 +1327,8 @@ __device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_
 // earlier blocks' output, contiguous when every one of them is full.
 // Returns the block's status code; out_len gets its output length.
 //
-// ZL (the linked path's second plane, k_decode_idx_zl): every literal byte
+// ZL (the linked path's second plane, k_decode_idx_zl; a constant at each
+// inlined call site, so the other decoders' code has none of it): every literal byte
 // is written as 0, so an output byte is nonzero only where it came from
 // the synthetic history (whose bytes there hold the history position's
 // high byte); a match reading history positions below 256 (more than
@@ -1345,14 +1336,13 @@ __device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_
 // AUX_DEEP_HIST; a stored block is all zeros; an oversized batch (literals
 // straight to HBM) declines the block, which then takes the three-plane
 // decode (lz4ada_bulk_linked.cpp).
-template <bool ZL = false>
 __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __restrict__ frame,
                                                 uint64_t frame_len,
                                                 const lz4ada_block_desc* __restrict__ desc,
                                                 uint32_t b, const uint8_t* __restrict__ tab_all,
                                                 uint8_t* __restrict__ out,
                                                 lz4ada_block_status* __restrict__ status,
-                                                int64_t hist, int32_t& out_len)
+                                                int64_t hist, int32_t& out_len, const bool ZL = false)
 {
 	const int32_t lane = int32_t(lane_id());
 	const lz4ada_block_desc d = desc[b];
@@ -1612,7 +1602,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #ifdef LZ4ADA_IDX_EXP_NOVG  // timing experiment: no HBM match loads (wrong output)
 							vg[r][c] = u32x4{uint32_t(src), 0u, 0u, 0u};
 #else
-							vg[r][c] = ldg16(ob + src + 16 * c);
+							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
 #endif
 					nc[r] = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
 					GCOUNT(0, __popcll(__ballot(g)));
@@ -1650,7 +1640,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #ifdef LZ4ADA_IDX_EXP_NOVG
 					vr = u32x4{uint32_t(od - ooff), 0u, 0u, 0u};
 #else
-					vr = ldg16(ob + (od - ooff) + 16 * k);
+					__builtin_memcpy(&vr, ob + (od - ooff) + 16 * k, 16);
 #endif
 				}
 				wave_lds_fence();  // ldesc / own[] are written again later
@@ -1750,7 +1740,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 						const int32_t oml = __shfl(ml, lo);
 						if (t < rtot[r]) {
 							u32x4 v;
-							v = ldg16(ob + osrc + 16 * k);
+							__builtin_memcpy(&v, ob + osrc + 16 * k, 16);
 							ostore(D, odst + 16 * k, v, min(16, oml - 16 * k));
 						}
 					}
@@ -1905,7 +1895,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	if (blockIdx.x >= nblocks)
 		return;
 	int32_t len;
-	decode_block<true>(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, LINK_HIST, len);
+	decode_block(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, LINK_HIST, len, true);
 }
 
 // ============================================================ two waves
