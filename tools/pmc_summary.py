@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile.sh run into profiles/.
+"""Summarise a tools/gpu_steps.sh pmc run (trace + one pass per counter group) into profiles/.
 
     python tools/pmc_summary.py gpurun_out/prof_r01 r01 [--kind mixed --blocks 2048]
 
@@ -147,7 +147,7 @@ def main():
               "avg_ns": dec.get("avg_ns"),
               # bench.py reuses the figure only while the kernel's machine code matches
               "kernel_code_sha16": "+".join(str(kernel_code_hash(k)) for k in dname.split("+")),
-              "source": f"profiles/{args.tag}_pmc.json (tools/profile.sh + tools/pmc_summary.py)"}
+              "source": f"profiles/{args.tag}_pmc.json (tools/gpu_steps.sh pmc + tools/pmc_summary.py)"}
         with open(os.path.join(prof, "pmc_decode.json"), "w") as fh:
             json.dump(pj, fh, indent=1)
     print(json.dumps({k: {kk: v for kk, v in e.items() if kk != "counters_per_dispatch"}
