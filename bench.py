@@ -568,8 +568,8 @@ def bench_facade(feed=4096, reps=5):
     driven from C the way tool_unlz4ada drives the library -- 4 KiB reads
     (tool_unlz4ada/unlz4ada.adb:16, 84-103), a context per frame -- on three
     frames with block and content checksums: 64 KiB independent blocks (the
-    LZ4F default block size), 256 KiB linked blocks, 4 MiB independent
-    blocks.  Each is timed next to the oracle's 1-core loop over the same
+    LZ4F default block size), 64 KiB linked blocks (the LZ4F default frame:
+    linked, 64 KiB), 256 KiB linked blocks, 4 MiB independent blocks.  Each is timed next to the oracle's 1-core loop over the same
     frame (the reference's CPU path, 4 KiB reads).  Host-resident input and
     output: this is the facade's latency path, not the bulk roofline."""
     import tempfile
@@ -579,8 +579,8 @@ def bench_facade(feed=4096, reps=5):
     import lz4frame
     exe = os.path.join(ROOT, "bo-lz4-ada_amd", "facade_bench")
     L = O.lib()
-    cases = [("indep_64k", 64 << 10, 64, True), ("linked_256k", 256 << 10, 32, False),
-             ("indep_4m", 4 << 20, 8, True)]
+    cases = [("indep_64k", 64 << 10, 64, True), ("linked_64k", 64 << 10, 64, False),
+             ("linked_256k", 256 << 10, 32, False), ("indep_4m", 4 << 20, 8, True)]
     rows = {}
     with tempfile.TemporaryDirectory() as td:
         for name, bmax, nb, indep in cases:
