@@ -578,8 +578,18 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
                                                    LoneCtl* __restrict__ ctl,
                                                    lz4ada_block_status* __restrict__ st,
                                                    uint32_t* __restrict__ Wbase, int32_t H,
-                                                   int32_t d1, int32_t n1)
+                                                   int32_t d1, int32_t n1, int32_t nwin,
+                                                   const uint8_t* __restrict__ h0, int32_t n0,
+                                                   const uint8_t* __restrict__ h1)
 {
+	// the workgroups past the windows write the history words (round 4: a
+	// launch of its own, k_lone_hist)
+	if (int32_t(blockIdx.x) >= nwin) {
+		for (int32_t i = (int32_t(blockIdx.x) - nwin) * LT * 4 + int32_t(threadIdx.x); i < H &&
+		     i < (int32_t(blockIdx.x) - nwin + 1) * LT * 4; i += LT)
+			Wbase[i] = LIT | uint32_t(i < n0 ? h0[i] : h1[i - n0]);
+		return;
+	}
 	// d1: 0, or 1 (decline every match >= D1_OFF back before the block), or
 	// the round's OPH (>= 65536: emulate quirk D1); n1: the block's position
 	// in the round (its history's current-round part)
@@ -871,18 +881,6 @@ __global__ __launch_bounds__(LT) void k_lone_resolve(uint32_t* __restrict__ W,
 	}
 }
 
-// History words: the H bytes before the block (a linked frame's earlier
-// output) as literals, so matches reaching back resolve like any other.
-__global__ __launch_bounds__(LT) void k_lone_hist(uint32_t* __restrict__ W, const uint8_t* __restrict__ h0,
-                                                  int32_t n0, const uint8_t* __restrict__ h1, int32_t n1)
-{
-	const int32_t i = int32_t(blockIdx.x) * LT + int32_t(threadIdx.x);
-	if (i < n0)
-		W[i] = LIT | uint32_t(h0[i]);
-	else if (i < n0 + n1)
-		W[i] = LIT | uint32_t(h1[i - n0]);
-}
-
 // ---------------------------------------------------------------- host side
 constexpr int64_t LONE_HDR = 256;  // the scratch's fixed header: the windows' done count
 
@@ -991,15 +989,10 @@ static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ad
 		if (err != hipSuccess)
 			return err;
 	}
-	if (H > 0) {
-		hipLaunchKernelGGL(k_lone_hist, dim3(uint32_t((H + LT - 1) / LT)), dim3(LT), 0, stream, W, d_h0,
-		                   n0, d_h1, n1);
-		err = hipGetLastError();
-		if (err != hipSuccess)
-			return err;
-	}
-	hipLaunchKernelGGL(k_lone_words<LW>, dim3(uint32_t(nwin)), dim3(LT), 0, stream, d_blk, int32_t(n),
-	                   nxt_tab, entry, obase, ctl, d_st, W, H, d1, n1);
+	// the history words ride in the words launch (workgroups past nwin)
+	const uint32_t nh = uint32_t((H + 4 * LT - 1) / (4 * LT));
+	hipLaunchKernelGGL(k_lone_words<LW>, dim3(uint32_t(nwin) + nh), dim3(LT), 0, stream, d_blk, int32_t(n),
+	                   nxt_tab, entry, obase, ctl, d_st, W, H, d1, n1, int32_t(nwin), d_h0, n0, d_h1);
 	return hipGetLastError();
 }
 
