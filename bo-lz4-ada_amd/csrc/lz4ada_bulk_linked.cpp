@@ -85,20 +85,27 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			return BULK_EXACT;
 		}
 		DevBuf<lz4ada_block_desc> d_desc;
-		DevBuf<lz4ada_block_status> sx, sz;
+		DevBuf<lz4ada_block_status> s2;  // planes x's and z's statuses, one copy back
 		d_desc.reserve(nb);
-		sx.reserve(nb);
-		sz.reserve(nb);
+		s2.reserve(2 * size_t(nb));
+		struct {
+			lz4ada_block_status* p;
+		} sx{ s2.p }, sz{ s2.p + nb };
 		const size_t sb = nb * sizeof(lz4ada_block_status);
+		// pinned: the statuses back, A and the modes out, without staging
+		PinBuf pin;
+		pin.reserve(2 * sb + nb * (sizeof(int64_t) + 1));
 		phase("alloc");
 		HIP_OK(hipMemcpyAsync(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc),
 		                      hipMemcpyHostToDevice, stream));
 		HIP_OK(hipMemsetAsync(sx.p, 0, sb, stream));
-		// the checksums ride beside the index and decodes (side stream),
-		// joined before the statuses are read
+		// the history regions' fill and the checksums ride beside the index
+		// (side stream); the decodes wait for the fill, the status read for
+		// the checksums
+		HIP_OK(launch_link_fill_beside(bx.p, nullptr, bz.p, d_desc.p, nb, stream));
 		HIP_OK(launch_block_checksums_beside(d_frame, d_desc.p, nb, sx.p, stream));
-		HIP_OK(launch_link_fill(bx.p, nullptr, bz.p, d_desc.p, nb, stream));
 		HIP_OK(launch_index(d_frame, frame_len, d_desc.p, nb, tab.p, sx.p, stream));
+		HIP_OK(join_link_fill(stream));
 		HIP_OK(hipMemcpyAsync(sz.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
 		HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bx.p, sx.p, 2, stream));
 		HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bx.p, sx.p, 1, LINK_HIST, stream));
@@ -106,9 +113,10 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		HIP_OK(join_block_checksums(stream));
 		phase("decodes");
 		std::vector<lz4ada_block_status> st(nb), stz(nb);
-		HIP_OK(hipMemcpyAsync(stz.data(), sz.p, sb, hipMemcpyDeviceToHost, stream));
-		d2h(st.data(), sx.p, sb, stream);
-		std::vector<int64_t> A(nb);
+		d2h(pin.p, s2.p, 2 * sb, stream);
+		memcpy(st.data(), pin.p, sb);
+		memcpy(stz.data(), pin.p + sb, sb);
+		int64_t* A = reinterpret_cast<int64_t*>(pin.p + 2 * sb);  // 8-aligned: sb is 32 nb
 		int64_t n = 0;
 		const int64_t opos0 = opos, oph0 = oph;  // this batch's start (a smaller retry rescans)
 		// the first block the exact path has to take: a block error, a
@@ -156,7 +164,8 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		// one z's decoder declined (oversized batches, anything pass 1
 		// declined) takes y and h -- the three-plane rule.  Every other block
 		// is DS_SKIP in those launches.
-		std::vector<uint8_t> mode(nb, 0);
+		uint8_t* mode = pin.p + 2 * sb + nb * sizeof(int64_t);
+		memset(mode, 0, nb);
 		uint32_t ny = 0, nh = 0;
 		for (uint32_t i = 0; i < nb; ++i) {
 			if (stz[i].code != DS_OK)
@@ -174,7 +183,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			if (!py || (nh && !ph))
 				return BULK_EXACT;
 			d_mode.reserve(nb);
-			HIP_OK(hipMemcpyAsync(d_mode.p, mode.data(), nb, hipMemcpyHostToDevice, stream));
+			HIP_OK(hipMemcpyAsync(d_mode.p, mode, nb, hipMemcpyHostToDevice, stream));
 			HIP_OK(launch_link_fill(nullptr, py, ph, d_desc.p, nb, stream));
 			std::vector<lz4ada_block_status> s_plane[2];
 			for (int k = 0; k < (nh ? 2 : 1); ++k) {
@@ -205,10 +214,9 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		if (!d_P.p)
 			return BULK_EXACT;
 		d_A.reserve(nb);
-		d_ctr.reserve(2);
-		HIP_OK(hipMemcpyAsync(d_A.p, A.data(), nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+		d_ctr.reserve(4);
+		HIP_OK(hipMemcpyAsync(d_A.p, A, nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
 		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
-		uint32_t ctr[2] = { 0, 0 };
 		uint8_t* F = nullptr;
 		// a word per output byte (resolving only the history-derived bytes,
 		// round 4's sparse form, measured slower -- three gathers per target
@@ -232,7 +240,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			// first round reads only those
 			HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
 			HIP_OK(launch_link_init(bx.p, bz.p, py, ph, ny ? d_mode.p : nullptr, d_desc.p, sx.p, d_A.p, nb,
-			                        block_max, d_P.p, F, act + ns, stream));
+			                        block_max, d_tail[cur].p, tail_valid, d_P.p, F, act + ns, stream));
 			phase("init");
 			auto spans_flagged = [&](const uint8_t* a) {  // (trace only) spans a round will visit
 				if (!trace)
@@ -245,22 +253,29 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				fprintf(stderr, "[linked] spans     %zu of %lld flagged\n", c, (long long)ns);
 			};
 			spans_flagged(act + ns);
-			// the first round always runs: init's span flags leave it nothing
-			// to read when no byte came from history (a count would cost an
-			// atomic per wave and a round trip)
-			ctr[0] = 1;
-			for (int round = 0; ctr[0] > 0; ++round) {
+			// the rounds run in pairs, one host round trip per pair (a mixed
+			// frame needs two rounds; a round after the last one finds every
+			// span flagged 0 and reads only the flags).  The first pair always
+			// runs: init's span flags leave it nothing to read when no byte
+			// came from history (a count would cost an atomic per wave and a
+			// round trip)
+			uint32_t left = 1;
+			for (int round = 0; left > 0; round += 2) {
 				if (round > 64)
 					return BULK_EXACT;  // never expected: every pointer goes strictly back
-				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 2 * sizeof(uint32_t), stream));
-				uint8_t* a_out = act + (round & 1) * ns;
-				const uint8_t* a_in = act + ((round + 1) & 1) * ns;
-				HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out, d_ctr.p,
-				                        stream));
-				d2h(ctr, d_ctr.p, sizeof ctr, stream);
-				spans_flagged(a_out);
-				if (ctr[1])
+				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 4 * sizeof(uint32_t), stream));
+				for (int k = 0; k < 2; ++k) {
+					uint8_t* a_out = act + ((round + k) & 1) * ns;
+					const uint8_t* a_in = act + ((round + k + 1) & 1) * ns;
+					HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out,
+					                        d_ctr.p + 2 * k, stream));
+					spans_flagged(a_out);
+				}
+				uint32_t c4[4];
+				d2h(c4, d_ctr.p, sizeof c4, stream);
+				if (c4[1] || c4[3])
 					return BULK_EXACT;  // a reference before the frame start: the exact error
+				left = c4[2];  // words still unresolved after the pair's second round
 			}
 			phase("jumps");
 		}

@@ -177,14 +177,22 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 hipError_t launch_block_checksums_beside(const uint8_t* d_frame, const lz4ada_block_desc* d_desc,
                                         uint32_t nblocks, lz4ada_block_status* d_status, hipStream_t stream);
 hipError_t join_block_checksums(hipStream_t stream);
+// k_link_fill on the same side stream (after everything already on
+// stream), so it runs beside k_index; join_link_fill makes stream wait for
+// it (before the decodes that read the history regions).
+hipError_t launch_link_fill_beside(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_block_desc* d_desc,
+                                   uint32_t nblocks, hipStream_t stream);
+hipError_t join_link_fill(hipStream_t stream);
 // Words from the planes: x (history k -> k & 255) and z (literals 0,
 // history k -> k >> 8) for every block; d_three (nullable) gives a block's
 // mode -- 1: y (~x) as well, 2: x, y and h (k >> 8) instead.
+// Each pointer is stepped once from its source's planes (d_tail: the
+// tail_valid bytes before the batch, for sources there).
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y, const uint8_t* h,
                             const uint8_t* d_three, const lz4ada_block_desc* d_desc,
                             const lz4ada_block_status* d_st, const int64_t* d_A, uint32_t nblocks,
-                            int64_t block_max, uint32_t* d_P, uint8_t* d_F, uint8_t* d_act,
-                            hipStream_t stream);
+                            int64_t block_max, const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_P,
+                            uint8_t* d_F, uint8_t* d_act, hipStream_t stream);
 // One pointer-jumping round; d_act_in (nullptr: every span) / d_act_out:
 // a byte per span of positions, 1 while the span holds an unresolved word.
 int64_t link_spans(int64_t n);

@@ -1465,7 +1465,7 @@ static int decoder_variant()
 // created on first use and kept for the process.
 struct SideStream {
 	hipStream_t s = nullptr;
-	hipEvent_t fork = nullptr, join = nullptr;
+	hipEvent_t fork = nullptr, join = nullptr, fill = nullptr;
 };
 
 static hipError_t side_stream(SideStream*& out)
@@ -1486,7 +1486,11 @@ static hipError_t side_stream(SideStream*& out)
 			err = hipEventCreateWithFlags(&n.fork, hipEventDisableTiming);
 		if (err == hipSuccess)
 			err = hipEventCreateWithFlags(&n.join, hipEventDisableTiming);
+		if (err == hipSuccess)
+			err = hipEventCreateWithFlags(&n.fill, hipEventDisableTiming);
 		if (err != hipSuccess) {
+			if (n.fill)
+				(void)hipEventDestroy(n.fill);
 			if (n.join)
 				(void)hipEventDestroy(n.join);
 			if (n.fork)
@@ -1522,6 +1526,29 @@ hipError_t join_block_checksums(hipStream_t stream)
 	SideStream* side = nullptr;
 	const hipError_t err = side_stream(side);
 	return err != hipSuccess ? err : hipStreamWaitEvent(stream, side->join, 0);
+}
+
+hipError_t launch_link_fill_beside(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_block_desc* d_desc,
+                                   uint32_t nblocks, hipStream_t stream)
+{
+	SideStream* side = nullptr;
+	hipError_t err = side_stream(side);
+	if (err == hipSuccess)
+		err = hipEventRecord(side->fork, stream);
+	if (err == hipSuccess)
+		err = hipStreamWaitEvent(side->s, side->fork, 0);
+	if (err == hipSuccess)
+		err = launch_link_fill(x, y, h, d_desc, nblocks, side->s);
+	if (err == hipSuccess)
+		err = hipEventRecord(side->fill, side->s);
+	return err;
+}
+
+hipError_t join_link_fill(hipStream_t stream)
+{
+	SideStream* side = nullptr;
+	const hipError_t err = side_stream(side);
+	return err != hipSuccess ? err : hipStreamWaitEvent(stream, side->fill, 0);
 }
 
 hipError_t launch_decode_checked(const uint8_t* d_frame, uint64_t frame_len,

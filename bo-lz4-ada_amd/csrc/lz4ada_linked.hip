@@ -11,13 +11,18 @@
 //    region (desc.out_off - 65536), so the decoders read "before the block
 //    start" like any other output byte (k_decode_idx mode 2, k_decode_pc
 //    with hist = LINK_HIST);
-//  * three decodes of the whole batch with different history patterns at
-//    position k of the region: X = k & 255, Y = ~X, H = k >> 8.  Decoding
-//    only moves bytes, so an output byte equal in X and Y is a constant (a
-//    literal, maybe copied on), and one that differs came from history
-//    position k = X | H << 8 -- byte (k - 65536) relative to its block start;
-//  * k_link_init turns the three outputs into one word per output byte, a
-//    resolved byte or a pointer to an earlier position of the frame;
+//  * two decodes of the whole batch with different history patterns at
+//    position k of the region: plane X holds k & 255 there; plane Z has
+//    every literal written as 0 and k >> 8 in the region.  Decoding only
+//    moves bytes, so a byte that is 0 in Z is a constant (a literal, maybe
+//    copied on) and any other came from history position k = X | Z << 8 --
+//    byte (k - 65536) relative to its block start.  Blocks that read
+//    history positions below 256 (their high byte is 0 too) or that Z's
+//    decoder declined also take Y = ~X (and H = k >> 8): the three-plane rule;
+//  * k_link_init turns the planes into one word per output byte, a
+//    resolved byte or a pointer to an earlier position of the frame, and
+//    takes each pointer one step already: the source byte's own planes
+//    (final before init runs) say whether it is a constant;
 //  * k_link_jump resolves the pointers by pointer jumping (each round
 //    replaces a pointer by its target's word, so chains through many
 //    blocks finish in ~log2(length) rounds), reading positions before the
@@ -92,9 +97,21 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 // A[b] + q): RES | byte, or the encoded position of the byte it copies,
 // (source position) + 65536 -- always >= 0, and below a.  Every byte also
 // goes to F (a history-derived one as a placeholder, rewritten by the jump
-// round that resolves it), so no emit pass reads the words again.  16 bytes
-// per lane: dwordx4 loads of the three copies, four 16-byte word stores.
+// round that resolves it), so no emit pass reads the words again.
+//
+// Each pointer is taken one step here already, from the planes of its
+// source byte (all final before this launch; the words of other blocks are
+// not: they are being written by this launch): a source in one of the
+// three blocks before b whose planes are x and z (mode 0) is a constant
+// (z = 0: its x byte) or a pointer one step further back; a source before
+// the batch is the tail's byte.  Anything else (a source further back, a
+// mode 1 / 2 block) keeps its pointer for the jump rounds.  On the bench's
+// linked frame that leaves the first round ~18% of the spans instead of
+// ~97%.
 constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
+#ifndef LZ4ADA_LINK_J_UNROLL
+#define LZ4ADA_LINK_J_UNROLL 1  // 0: a lane's four quads one after the other (fewer registers)
+#endif
 
 __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x,
                                                    const uint8_t* __restrict__ z,
@@ -104,6 +121,7 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
                                                    const lz4ada_block_desc* __restrict__ desc,
                                                    const lz4ada_block_status* __restrict__ st,
                                                    const int64_t* __restrict__ A, uint32_t nblocks,
+                                                   const uint8_t* __restrict__ tail, int32_t tail_valid,
                                                    uint32_t* __restrict__ P, uint8_t* __restrict__ F,
                                                    uint8_t* __restrict__ act)
 {
@@ -126,6 +144,18 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 	const bool tri = md != 0;
 	const uint8_t* __restrict__ y = tri ? y3 : z;
 	const uint8_t* __restrict__ h = md == 2 ? h3 : z;
+	// the three blocks before b (a source is at most 65535 bytes back):
+	// batch position (INT32_MAX: none, or not mode 0) and slot
+	int32_t pa[3];
+	uint64_t po[3];
+	bool more = true;  // stop at the first block before b that is not mode 0
+#pragma unroll
+	for (int r = 0; r < 3; ++r) {
+		const int32_t bb = int32_t(b) - 1 - r;
+		more = more && bb >= 0 && (!three || three[bb] == 0);
+		pa[r] = more ? int32_t(A[bb]) : INT32_MAX;
+		po[r] = more ? desc[bb].out_off : 0;
+	}
 	// a wave takes 1 KiB of the block at a time, lane l its bytes g0 + 4 l +
 	// 256 j (j < 4): every load (a dword of each copy), word store (16 bytes)
 	// and byte store (a dword) of the wave is one contiguous run (round 4
@@ -155,13 +185,18 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 		// the spans (SPAN positions each) this wave's kilobyte meets: at most two
 		const int64_t sA = (ab + g0) / SPAN;
 		bool inA = false, inB = false;
+		auto which = [&](int32_t t) { return t >= pa[0] ? 0 : (t >= pa[1] ? 1 : (t >= pa[2] ? 2 : 3)); };
+#if LZ4ADA_LINK_J_UNROLL
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
 		for (int j = 0; j < 4; ++j) {
 			const int64_t q = g0 + 256 * j + 4 * lane;
 			const int32_t nv = int32_t(min<int64_t>(4, max<int64_t>(len - q, 0)));
-			// branch-free per byte; positions fit 31 bits (bulk_linked checks),
-			// so the words are 32-bit sums
-			uint32_t v[4], u = 0;
+			// words: branch-free per byte; positions fit 31 bits (bulk_linked
+			// checks), so the words are 32-bit sums
+			uint32_t v[4];
 #pragma unroll
 			for (int i = 0; i < 4; ++i) {
 				const uint32_t bx = (wx[j] >> (8 * i)) & 255u;
@@ -171,7 +206,47 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 				const uint32_t hist = (from_hist && i < nv) ? 0xFFFFFFFFu : 0u;
 				const uint32_t lit = RES | bx, ptr = hb + (bx | (bh << 8));
 				v[i] = lit ^ ((lit ^ ptr) & hist);
-				u += hist & 1u;
+			}
+			// one step of every pointer: its source's planes (or the tail's
+			// byte), the loads issued before any is used (loading a quad's
+			// four consecutive source bytes as two dwords per plane instead
+			// measured slower: mixed init 2.17 -> 2.60 ms)
+			uint32_t sx[4], sz[4];
+#pragma unroll
+			for (int i = 0; i < 4; ++i) {
+				sx[i] = 0;
+				sz[i] = 1;
+				if (v[i] & RES)
+					continue;
+				const int32_t t = int32_t(v[i]) - int32_t(HISTORY_SIZE);
+				if (t < 0) {
+					if (t >= -tail_valid) {
+						sx[i] = tail[HISTORY_SIZE + t];
+						sz[i] = 0;
+					}
+				} else {
+					const int r = which(t);
+					if (r < 3) {
+						const uint64_t o = (r == 0 ? po[0] : (r == 1 ? po[1] : po[2])) +
+						                   uint64_t(t - (r == 0 ? pa[0] : (r == 1 ? pa[1] : pa[2])));
+						sx[i] = x[o];
+						sz[i] = z[o];
+					}
+				}
+			}
+			uint32_t u = 0;
+#pragma unroll
+			for (int i = 0; i < 4; ++i) {
+				if (!(v[i] & RES)) {
+					const int32_t t = int32_t(v[i]) - int32_t(HISTORY_SIZE);
+					const int r = which(t);
+					const uint32_t base = uint32_t(r == 0 ? pa[0] : (r == 1 ? pa[1] : pa[2]));
+					if (sz[i] == 0)
+						v[i] = RES | sx[i];  // a constant (or the tail's byte)
+					else if (t >= 0 && r < 3)
+						v[i] = base + (sx[i] | (sz[i] << 8));  // its source's own pointer
+				}
+				u += (v[i] & RES) ? 0u : 1u;
 			}
 			if (u) {  // the first jump round visits only the spans flagged here
 				inA |= (ab + q) / SPAN == sA;
@@ -200,81 +275,101 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 
 // One pointer-jumping round over P[0, n).  ctr[0] = 1: a word is still
 // unresolved after the round; ctr[1] = 1: a reference before the frame
-// start (a position below -tail_valid).  tail: the 65536 output bytes before the batch.  A
-// lane takes four positions: their words, then every unresolved one's
-// target word, loaded together before any is used; where a word changes the
-// lane rewrites its four bytes of F (the last round to touch them leaves the
-// final bytes).
+// start (a position below -tail_valid).  tail: the 65536 output bytes
+// before the batch.  Every unresolved word is replaced by its target's
+// word; where a word changes, its four-byte group of F is rewritten (the
+// last round to touch them leaves the final bytes).
 //
-// Activity flags: a workgroup pass covers SPAN consecutive positions; act_out
-// gets 1 for a span that still holds an unresolved word after the round, and
-// a later round given act_in skips every span flagged 0 (most of the frame
-// after the first round) instead of reading its words again.
+// Activity flags: one per SPAN consecutive positions; act_out gets 1 for a
+// span that still holds an unresolved word after the round, and a later
+// round given act_in skips every span flagged 0 (most of the frame after
+// the first round) instead of reading its words again.
 
-// Positions a0 .. a0+3 (a0 < n): one jump of every unresolved word, their
-// bytes to F.  Returns the words still unresolved.
-__device__ __forceinline__ uint32_t jump4(GLOBAL uint32_t* Pg, int64_t a0, int64_t n,
-                                          const uint8_t* __restrict__ tail, int64_t tail_valid,
-                                          uint8_t* __restrict__ F, uint32_t& bad)
+// A whole span (SPAN positions) in one wave: lane l takes positions s0 +
+// 256 j + 4 l + i (j, i < 4).  All four word loads are issued before any is
+// used, then every unresolved word's target together: four times the loads
+// in flight of round 4's quad per thread, the round's limit (a round is two
+// dependent memory trips per span).  Returns the words still unresolved.
+__device__ __forceinline__ uint32_t jump_span(GLOBAL uint32_t* Pg, int64_t s0, int64_t n,
+                                              const uint8_t* __restrict__ tail, int64_t tail_valid,
+                                              uint8_t* __restrict__ F, uint32_t& bad)
 {
-	uint32_t w[4];
-	const bool full = a0 + 4 <= n;
-	if (full) {
-		const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(Pg + a0);
-		w[0] = v.x;
-		w[1] = v.y;
-		w[2] = v.z;
-		w[3] = v.w;
-	} else {
+	const int64_t l4 = 4 * int64_t(lane_id());
+	uint32_t w[16];
 #pragma unroll
-		for (int i = 0; i < 4; ++i)
-			w[i] = a0 + i < n ? Pg[a0 + i] : RES;
+	for (int j = 0; j < 4; ++j) {
+		const int64_t a0 = s0 + 256 * j + l4;
+		if (a0 + 4 <= n) {
+			const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(Pg + a0);
+			w[4 * j] = v.x;
+			w[4 * j + 1] = v.y;
+			w[4 * j + 2] = v.z;
+			w[4 * j + 3] = v.w;
+		} else {
+#pragma unroll
+			for (int i = 0; i < 4; ++i)
+				w[4 * j + i] = a0 + i < n ? Pg[a0 + i] : RES;
+		}
 	}
-	if ((w[0] & w[1] & w[2] & w[3]) & RES)
-		return 0;  // all resolved (their bytes are in F already)
-	uint32_t f[4];
+	uint32_t all = RES;
 #pragma unroll
-	for (int i = 0; i < 4; ++i) {
-		const int64_t t = int64_t(w[i] & ~RES) - HISTORY_SIZE;
-		f[i] = w[i];
-		if (w[i] & RES)
+	for (int k = 0; k < 16; ++k)
+		all &= w[k];
+	if (all & RES)
+		return 0;  // all resolved (their bytes are in F already)
+	uint32_t f[16];
+#pragma unroll
+	for (int k = 0; k < 16; ++k) {
+		const int64_t t = int64_t(w[k] & ~RES) - HISTORY_SIZE;
+		f[k] = w[k];
+		if (w[k] & RES)
 			continue;
 		if (t >= 0)
-			f[i] = Pg[t];  // the source's word: resolved, or a pointer further back
+			f[k] = Pg[t];  // the source's word: resolved, or a pointer further back
 		else if (t >= -tail_valid)
-			f[i] = RES | tail[HISTORY_SIZE + t];
+			f[k] = RES | tail[HISTORY_SIZE + t];
 		else
-			f[i] = ~0u;  // before the frame start
+			f[k] = ~0u;  // before the frame start
 	}
-	uint32_t o = 0, unres = 0;
+	uint32_t unres = 0;
 #pragma unroll
-	for (int i = 0; i < 4; ++i) {
-		if (f[i] == ~0u) {
-			++bad;
-			f[i] = w[i];
+	for (int j = 0; j < 4; ++j) {
+		const int64_t a0 = s0 + 256 * j + l4;
+		if ((w[4 * j] & w[4 * j + 1] & w[4 * j + 2] & w[4 * j + 3]) & RES)
+			continue;  // this quad was resolved: F has its bytes
+		uint32_t o = 0;
+#pragma unroll
+		for (int i = 0; i < 4; ++i) {
+			uint32_t& x = f[4 * j + i];
+			if (x == ~0u) {
+				++bad;
+				x = w[4 * j + i];
+			}
+			if (x != w[4 * j + i])
+				Pg[a0 + i] = x;
+			unres += (x & RES) ? 0u : 1u;
+			o |= (x & 255u) << (8 * i);
 		}
-		if (f[i] != w[i])
-			Pg[a0 + i] = f[i];
-		unres += (f[i] & RES) ? 0u : 1u;
-		o |= (f[i] & 255u) << (8 * i);
-	}
-	GLOBAL uint8_t* fb = gptr(F) + a0;
-	if (full && (reinterpret_cast<uintptr_t>(fb) & 3u) == 0) {
-		*reinterpret_cast<GLOBAL uint32_t*>(fb) = o;
-	} else {
+		GLOBAL uint8_t* fb = gptr(F) + a0;
+		if (a0 + 4 <= n && (reinterpret_cast<uintptr_t>(fb) & 3u) == 0) {
+			*reinterpret_cast<GLOBAL uint32_t*>(fb) = o;
+		} else {
 #pragma unroll
-		for (int i = 0; i < 4; ++i)
-			if (a0 + i < n)
-				fb[i] = uint8_t(o >> (8 * i));
+			for (int i = 0; i < 4; ++i)
+				if (a0 + i < n)
+					fb[i] = uint8_t(o >> (8 * i));
+		}
 	}
 	return unres;
 }
 
-// A workgroup takes SPW consecutive spans: it loads their SPW activity
-// flags at once (one coalesced load), then visits only the active ones --
-// round 4 read each span's flag in its loop, one dependent load per span,
-// which made a round that skips 94% of the spans cost 0.5 ms.
-constexpr int32_t SPW = TPB;  // spans per workgroup
+// Each wave takes 64 consecutive spans at a time: one coalesced load of
+// their activity flags, then only the active ones, a span per step with no
+// workgroup barrier (round 4 read each span's flag in its loop, one
+// dependent load per span, which made a round that skips 94% of the spans
+// cost 0.5 ms; until late round 5 a span was one quad per thread of the
+// workgroup, a __syncthreads per span).
+constexpr int32_t SPW = TPB;  // spans per workgroup pass (64 per wave)
 
 __global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int64_t n,
                                                    const uint8_t* __restrict__ tail,
@@ -283,32 +378,24 @@ __global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int
                                                    uint8_t* __restrict__ act_out,
                                                    uint32_t* __restrict__ ctr)
 {
-	__shared__ uint64_t on[SPW / 64];
 	uint32_t unres = 0, bad = 0;
 	GLOBAL uint32_t* Pg = gptr(P);
 	const int64_t nsp = (n + SPAN - 1) / SPAN;
-	const int32_t tid = int32_t(threadIdx.x);
-	for (int64_t sb = int64_t(blockIdx.x) * SPW; sb < nsp; sb += int64_t(gridDim.x) * SPW) {
-		const int64_t my = sb + tid;
+	const int32_t lane = int32_t(lane_id());
+	const int64_t w0 = int64_t(blockIdx.x) * SPW + 64 * int64_t(threadIdx.x >> 6);
+	for (int64_t sb = w0; sb < nsp; sb += int64_t(gridDim.x) * SPW) {
+		const int64_t my = sb + lane;
 		const bool a = my < nsp && (!act_in || act_in[my]);
-		const uint64_t m = __ballot(a);
-		if (lane_id() == 0)
-			on[tid >> 6] = m;
 		if (my < nsp && !a)
 			act_out[my] = 0;
-		__syncthreads();
-		for (int q = 0; q < SPW / 64; ++q) {
-			for (uint64_t mm = on[q]; mm; mm &= mm - 1) {
-				const int64_t span = sb + 64 * q + __builtin_ctzll(mm);
-				const int64_t a0 = span * SPAN + 4 * int64_t(tid);
-				const uint32_t u = a0 < n ? jump4(Pg, a0, n, tail, tail_valid, F, bad) : 0u;
-				unres += u;
-				const int any = __syncthreads_or(u != 0);
-				if (tid == 0)
-					act_out[span] = uint8_t(any);
-			}
+		for (uint64_t mm = __ballot(a); mm; mm &= mm - 1) {
+			const int64_t span = sb + __builtin_ctzll(mm);
+			const uint32_t u = jump_span(Pg, span * SPAN, n, tail, tail_valid, F, bad);
+			unres += u;
+			const bool any = __ballot(u != 0) != 0;
+			if (lane == 0)
+				act_out[span] = uint8_t(any);
 		}
-		__syncthreads();  // on[] is rewritten for the next spans
 	}
 	flag_any(&ctr[0], unres != 0);
 	flag_any(&ctr[1], bad != 0);
@@ -342,8 +429,8 @@ hipError_t launch_link_fill(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_blo
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y, const uint8_t* h,
                             const uint8_t* d_three, const lz4ada_block_desc* d_desc,
                             const lz4ada_block_status* d_st, const int64_t* d_A, uint32_t nblocks,
-                            int64_t block_max, uint32_t* d_P, uint8_t* d_F, uint8_t* d_act,
-                            hipStream_t stream)
+                            int64_t block_max, const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_P,
+                            uint8_t* d_F, uint8_t* d_act, hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
@@ -352,7 +439,7 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y
 	const int64_t per = 4 * 16 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
 	hipLaunchKernelGGL(link::k_link_init, dim3(gy, nblocks), dim3(link::TPB), 0, stream, x, z, y, h, d_three,
-	                   d_desc, d_st, d_A, nblocks, d_P, d_F, d_act);
+	                   d_desc, d_st, d_A, nblocks, d_tail, int32_t(tail_valid), d_P, d_F, d_act);
 	return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@
 #   facade   bo-lz4-ada_amd/facade_bench on 64 KiB / 256 KiB linked / 4 MiB frames, 4 KiB reads,
 #            with the facade's per-step laps (LZ4ADA_TRACE_FACADE) of the 64 KiB frame
 #   lone     tools/lone_time.py over block sizes and classes
-#   linked   tools/linked_time.py (configs[4] phases)
+#   linked   tools/linked_time.py (configs[4]: mixed, dense, chain; then the mixed phases)
 #   classes  tools/time_decode.py per content class (decoder alone and product step)
 #   pp2      the pipelined two-wave decoder: its parity tests, then timed beside
 #            k_decode_idx2 / k_decode_idx at 1,024 and 2,048 blocks
@@ -61,8 +61,13 @@ for step in "$@"; do
     timeout -k 10 400 python tools/lone_time.py > $O/${TAG}_lone.txt 2>&1 || fail lone $O/${TAG}_lone.txt
     grep -v amdgpu $O/${TAG}_lone.txt ;;
   linked)
-    timeout -k 10 400 python tools/linked_time.py > $O/${TAG}_linked.txt 2>&1 || fail linked $O/${TAG}_linked.txt
-    grep -v amdgpu $O/${TAG}_linked.txt ;;
+    for k in mixed dense chain; do
+      timeout -k 10 300 python tools/linked_time.py $k >> $O/${TAG}_linked.txt 2>&1 || fail linked $O/${TAG}_linked.txt
+    done
+    LZ4ADA_TRACE_LINKED=1 timeout -k 10 300 python tools/linked_time.py mixed > $O/${TAG}_linked_phases.txt 2>&1 \
+      || fail linked-phases $O/${TAG}_linked_phases.txt
+    grep -v amdgpu $O/${TAG}_linked.txt
+    tail -14 $O/${TAG}_linked_phases.txt ;;
   classes)
     for k in mixed dense literal rle; do
       timeout -k 10 200 python tools/time_decode.py --kind $k --variant idx1,product 2>&1 | grep -v amdgpu || fail classes /dev/null
