@@ -24,21 +24,42 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 	// a batch holds 3 decode buffers (slots + 64 KiB regions) and one 4-byte
 	// word per output byte: ~7x its slot bytes
 	uint64_t budget = uint64_t(env_bytes("LZ4ADA_LINKED_BATCH_BYTES", int64_t(2) << 30));
-	// LZ4ADA_TRACE_LINKED=1: phase times (synchronised) to stderr
-	static const bool trace = getenv("LZ4ADA_TRACE_LINKED") != nullptr;
+	// LZ4ADA_TRACE_LINKED=1: phase times (synchronised) to stderr; =2: the
+	// host's own time between the phases (no synchronisation)
+	static const int trace = [] {
+		const char* e = getenv("LZ4ADA_TRACE_LINKED");
+		return e ? std::max(1, atoi(e)) : 0;
+	}();
 	auto t0 = std::chrono::steady_clock::now();
 	auto phase = [&](const char* name) {
 		if (!trace)
 			return;
-		HIP_OK(hipStreamSynchronize(stream));
+		if (trace == 1)
+			HIP_OK(hipStreamSynchronize(stream));
 		const auto t1 = std::chrono::steady_clock::now();
 		fprintf(stderr, "[linked] %-10s %8.3f ms\n", name,
 		        std::chrono::duration<double, std::milli>(t1 - t0).count());
 		t0 = t1;
 	};
-	DevBuf<uint8_t> d_tail[2];
-	d_tail[0].reserve(size_t(HISTORY_SIZE));
-	d_tail[1].reserve(size_t(HISTORY_SIZE));
+	// the small per-call buffers -- both history tails, and per batch the
+	// descriptors, both planes' statuses, A, the modes and the round counters
+	// -- carved from one thread-cached device buffer, and their host sides
+	// from one thread-cached pinned buffer: a pooled buffer's release costs
+	// a device synchronisation (round 5: ~8 per call)
+	const size_t nmax = descs.size();
+	auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+	const size_t o_desc = 2 * size_t(HISTORY_SIZE), o_st = o_desc + al(nmax * sizeof(lz4ada_block_desc)),
+	             o_A = o_st + al(2 * nmax * sizeof(lz4ada_block_status)), o_mode = o_A + al(nmax * sizeof(int64_t)),
+	             o_ctr = o_mode + al(nmax), link_bytes = o_ctr + 256;
+	uint8_t* const lk = scratch(SC_LINK, link_bytes);
+	if (!lk)
+		return BULK_EXACT;
+	PinBuf& pin = scratch_cache().pin;
+	pin.reserve(link_bytes);
+	uint8_t* const hp = pin.p;  // host twin of lk: hp + o is the host side of lk + o
+	struct {
+		uint8_t* p;
+	} d_tail[2]{ { lk }, { lk + HISTORY_SIZE } };
 	HIP_OK(hipMemsetAsync(d_tail[0].p, 0, size_t(HISTORY_SIZE), stream));
 	int cur = 0;
 	// the reference's Output_Pos / Output_Pos_History (lz4ada.adb:678-690,
@@ -64,6 +85,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		const uint32_t hi = lo + bt[0].second;
 		uint32_t nb = hi - lo;
 		std::vector<lz4ada_block_desc> d(descs.begin() + lo, descs.begin() + hi);
+		phase("batch");
 		uint64_t bytes = 0;
 		for (auto& x : d) {
 			x.out_cap = slot_cap(x, block_max);
@@ -84,20 +106,19 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			}
 			return BULK_EXACT;
 		}
-		DevBuf<lz4ada_block_desc> d_desc;
-		DevBuf<lz4ada_block_status> s2;  // planes x's and z's statuses, one copy back
-		d_desc.reserve(nb);
-		s2.reserve(2 * size_t(nb));
+		// planes x's and z's statuses side by side: one copy back
+		struct {
+			lz4ada_block_desc* p;
+		} d_desc{ reinterpret_cast<lz4ada_block_desc*>(lk + o_desc) };
 		struct {
 			lz4ada_block_status* p;
-		} sx{ s2.p }, sz{ s2.p + nb };
+		} s2{ reinterpret_cast<lz4ada_block_status*>(lk + o_st) }, sx{ s2.p }, sz{ s2.p + nb };
 		const size_t sb = nb * sizeof(lz4ada_block_status);
-		// pinned: the statuses back, A and the modes out, without staging
-		PinBuf pin;
-		pin.reserve(2 * sb + nb * (sizeof(int64_t) + 1));
+		const size_t db = nb * sizeof(lz4ada_block_desc);
 		phase("alloc");
-		HIP_OK(hipMemcpyAsync(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc),
-		                      hipMemcpyHostToDevice, stream));
+		memcpy(hp + o_desc, d.data(), db);
+		HIP_OK(hipMemcpyAsync(d_desc.p, hp + o_desc, db, hipMemcpyHostToDevice, stream));
+		phase("desc h2d");
 		HIP_OK(hipMemsetAsync(sx.p, 0, sb, stream));
 		// the history regions' fill and the checksums ride beside the index
 		// (side stream); the decodes wait for the fill, the status read for
@@ -106,17 +127,26 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		HIP_OK(launch_block_checksums_beside(d_frame, d_desc.p, nb, sx.p, stream));
 		HIP_OK(launch_index(d_frame, frame_len, d_desc.p, nb, tab.p, sx.p, stream));
 		HIP_OK(join_link_fill(stream));
+		phase("launches");
 		HIP_OK(hipMemcpyAsync(sz.p, sx.p, sb, hipMemcpyDeviceToDevice, stream));
+		// plane z's decode on the side stream beside plane x's: each launch
+		// has more blocks than resident slots, and the other one's blocks
+		// fill the slots its last ones leave idle
+		// (LZ4ADA_LINK_SERIAL=1: one after the other, for A/B)
+		static const bool serial = getenv("LZ4ADA_LINK_SERIAL") != nullptr;
+		hipStream_t side = stream;
+		if (!serial)
+			HIP_OK(side_fork(stream, &side));
+		HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bz.p, sz.p, 6, side));
 		HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bx.p, sx.p, 2, stream));
 		HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, bx.p, sx.p, 1, LINK_HIST, stream));
-		HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, bz.p, sz.p, 6, stream));
-		HIP_OK(join_block_checksums(stream));
+		HIP_OK(side_join(stream));  // plane z and the checksums
 		phase("decodes");
 		std::vector<lz4ada_block_status> st(nb), stz(nb);
-		d2h(pin.p, s2.p, 2 * sb, stream);
-		memcpy(st.data(), pin.p, sb);
-		memcpy(stz.data(), pin.p + sb, sb);
-		int64_t* A = reinterpret_cast<int64_t*>(pin.p + 2 * sb);  // 8-aligned: sb is 32 nb
+		d2h(hp + o_st, s2.p, 2 * sb, stream);
+		memcpy(st.data(), hp + o_st, sb);
+		memcpy(stz.data(), hp + o_st + sb, sb);
+		int64_t* A = reinterpret_cast<int64_t*>(hp + o_A);
 		int64_t n = 0;
 		const int64_t opos0 = opos, oph0 = oph;  // this batch's start (a smaller retry rescans)
 		// the first block the exact path has to take: a block error, a
@@ -164,7 +194,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		// one z's decoder declined (oversized batches, anything pass 1
 		// declined) takes y and h -- the three-plane rule.  Every other block
 		// is DS_SKIP in those launches.
-		uint8_t* mode = pin.p + 2 * sb + nb * sizeof(int64_t);
+		uint8_t* mode = hp + o_mode;
 		memset(mode, 0, nb);
 		uint32_t ny = 0, nh = 0;
 		for (uint32_t i = 0; i < nb; ++i) {
@@ -176,13 +206,14 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			nh += mode[i] == 2;
 		}
 		uint8_t *py = nullptr, *ph = nullptr;
-		DevBuf<uint8_t> d_mode;
+		struct {
+			uint8_t* p;
+		} d_mode{ lk + o_mode };
 		if (ny) {
 			py = scratch(SC_Y, size_t(bytes));
 			ph = py && nh ? scratch(SC_H, size_t(bytes)) : nullptr;
 			if (!py || (nh && !ph))
 				return BULK_EXACT;
-			d_mode.reserve(nb);
 			HIP_OK(hipMemcpyAsync(d_mode.p, mode, nb, hipMemcpyHostToDevice, stream));
 			HIP_OK(launch_link_fill(nullptr, py, ph, d_desc.p, nb, stream));
 			std::vector<lz4ada_block_status> s_plane[2];
@@ -206,15 +237,17 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			}
 			phase("more planes");
 		}
-		DevBuf<int64_t> d_A;
-		DevBuf<uint32_t> d_ctr;
+		struct {
+			int64_t* p;
+		} d_A{ reinterpret_cast<int64_t*>(lk + o_A) };
+		struct {
+			uint32_t* p;
+		} d_ctr{ reinterpret_cast<uint32_t*>(lk + o_ctr) };
 		struct {
 			uint32_t* p;
 		} d_P{ reinterpret_cast<uint32_t*>(scratch(SC_P, size_t(std::max<int64_t>(n, 1)) * 4)) };
 		if (!d_P.p)
 			return BULK_EXACT;
-		d_A.reserve(nb);
-		d_ctr.reserve(4);
 		HIP_OK(hipMemcpyAsync(d_A.p, A, nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
 		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
 		uint8_t* F = nullptr;
@@ -271,15 +304,17 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 					                        d_ctr.p + 2 * k, stream));
 					spans_flagged(a_out);
 				}
-				uint32_t c4[4];
-				d2h(c4, d_ctr.p, sizeof c4, stream);
+				// the next batch's history, enqueued before the round trip (a
+				// later pair, if any, writes it again)
+				HIP_OK(launch_link_tail(F, n, d_tail[cur].p, d_tail[cur ^ 1].p, stream));
+				uint32_t* c4 = reinterpret_cast<uint32_t*>(hp + o_ctr);
+				d2h(c4, d_ctr.p, 4 * sizeof(uint32_t), stream);
 				if (c4[1] || c4[3])
 					return BULK_EXACT;  // a reference before the frame start: the exact error
 				left = c4[2];  // words still unresolved after the pair's second round
 			}
 			phase("jumps");
 		}
-		HIP_OK(launch_link_tail(F, n, d_tail[cur].p, d_tail[cur ^ 1].p, stream));
 		cur ^= 1;
 		phase("emit");
 		sink.done(F, n);

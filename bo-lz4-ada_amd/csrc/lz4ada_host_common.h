@@ -267,14 +267,18 @@ struct PinBuf {
 	PinBuf() = default;
 	PinBuf(const PinBuf&) = delete;
 	PinBuf& operator=(const PinBuf&) = delete;
-	~PinBuf() { pin_pool().put(p, bytes, dev); }
+	~PinBuf() { release(); }
+	void release()
+	{
+		pin_pool().put(p, bytes, dev);
+		p = nullptr;
+		n = bytes = 0;
+	}
 	void reserve(size_t count)
 	{
 		if (count <= n && p)
 			return;
-		pin_pool().put(p, bytes, dev);
-		p = nullptr;
-		n = bytes = 0;
+		release();
 		const auto b = pin_pool().get(std::max<size_t>(count, 1));
 		p = static_cast<uint8_t*>(b.p);
 		bytes = b.bytes;
@@ -725,9 +729,11 @@ inline bool try_reserve(DevBuf<T>& b, size_t count)
 // and a first-touch each time otherwise -- more than the decode itself on a
 // 1 GiB linked frame.  lz4ada_release_device_cache() frees them.  The
 // cache is never destroyed at thread exit (the HIP runtime may be gone).
-enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_Z, SC_TAB, SC_P, SC_F, SC_LONE, SC_U, SC_N };
+enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_Z, SC_TAB, SC_P, SC_F, SC_LONE, SC_U,
+	           SC_LINK, SC_N };
 struct ScratchCache {
 	DevBuf<uint8_t> b[SC_N];
+	PinBuf pin;  // the linked path's small host transfers (pinned: no staging copy)
 };
 inline ScratchCache& scratch_cache()
 {
@@ -738,6 +744,7 @@ inline void scratch_release()
 {
 	for (auto& x : scratch_cache().b)
 		x.release();
+	scratch_cache().pin.release();
 }
 // bytes of scratch `role`, or nullptr when the device has no room (the
 // caller then shrinks its batch or takes the exact path; other roles may be

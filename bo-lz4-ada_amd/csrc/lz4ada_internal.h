@@ -183,6 +183,11 @@ hipError_t join_block_checksums(hipStream_t stream);
 hipError_t launch_link_fill_beside(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_block_desc* d_desc,
                                    uint32_t nblocks, hipStream_t stream);
 hipError_t join_link_fill(hipStream_t stream);
+// The same side stream for any launch: side_fork gives it, ordered after
+// everything already on stream; side_join makes stream wait for everything
+// on it so far (the checksums included).
+hipError_t side_fork(hipStream_t stream, hipStream_t* side);
+hipError_t side_join(hipStream_t stream);
 // Words from the planes: x (history k -> k & 255) and z (literals 0,
 // history k -> k >> 8) for every block; d_three (nullable) gives a block's
 // mode -- 1: y (~x) as well, 2: x, y and h (k >> 8) instead.

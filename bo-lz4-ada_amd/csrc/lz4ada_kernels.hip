@@ -1528,6 +1528,28 @@ hipError_t join_block_checksums(hipStream_t stream)
 	return err != hipSuccess ? err : hipStreamWaitEvent(stream, side->join, 0);
 }
 
+hipError_t side_fork(hipStream_t stream, hipStream_t* side_s)
+{
+	SideStream* side = nullptr;
+	hipError_t err = side_stream(side);
+	if (err == hipSuccess)
+		err = hipEventRecord(side->fork, stream);
+	if (err == hipSuccess)
+		err = hipStreamWaitEvent(side->s, side->fork, 0);
+	if (err == hipSuccess)
+		*side_s = side->s;
+	return err;
+}
+
+hipError_t side_join(hipStream_t stream)
+{
+	SideStream* side = nullptr;
+	hipError_t err = side_stream(side);
+	if (err == hipSuccess)
+		err = hipEventRecord(side->join, side->s);
+	return err != hipSuccess ? err : hipStreamWaitEvent(stream, side->join, 0);
+}
+
 hipError_t launch_link_fill_beside(uint8_t* x, uint8_t* y, uint8_t* h, const lz4ada_block_desc* d_desc,
                                    uint32_t nblocks, hipStream_t stream)
 {
