@@ -109,6 +109,9 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 // linked frame that leaves the first round ~18% of the spans instead of
 // ~97%.
 constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
+#ifndef LZ4ADA_LINK_STEPS
+#define LZ4ADA_LINK_STEPS 2  // pointer steps taken in init from the planes
+#endif
 #ifndef LZ4ADA_LINK_J_UNROLL
 #define LZ4ADA_LINK_J_UNROLL 1  // 0: a lane's four quads one after the other (fewer registers)
 #endif
@@ -207,37 +210,39 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 				const uint32_t lit = RES | bx, ptr = hb + (bx | (bh << 8));
 				v[i] = lit ^ ((lit ^ ptr) & hist);
 			}
-			// one step of every pointer: its source's planes (or the tail's
-			// byte), the loads issued before any is used (loading a quad's
-			// four consecutive source bytes as two dwords per plane instead
-			// measured slower: mixed init 2.17 -> 2.60 ms)
-			uint32_t sx[4], sz[4];
+			// LZ4ADA_LINK_STEPS steps of every pointer: its source's planes (or
+			// the tail's byte), a step's loads issued before any is used
+			// (loading a quad's four consecutive source bytes as two dwords per
+			// plane instead measured slower: mixed init 2.17 -> 2.60 ms)
 #pragma unroll
-			for (int i = 0; i < 4; ++i) {
-				sx[i] = 0;
-				sz[i] = 1;
-				if (v[i] & RES)
-					continue;
-				const int32_t t = int32_t(v[i]) - int32_t(HISTORY_SIZE);
-				if (t < 0) {
-					if (t >= -tail_valid) {
-						sx[i] = tail[HISTORY_SIZE + t];
-						sz[i] = 0;
-					}
-				} else {
-					const int r = which(t);
-					if (r < 3) {
-						const uint64_t o = (r == 0 ? po[0] : (r == 1 ? po[1] : po[2])) +
-						                   uint64_t(t - (r == 0 ? pa[0] : (r == 1 ? pa[1] : pa[2])));
-						sx[i] = x[o];
-						sz[i] = z[o];
+			for (int stp = 0; stp < LZ4ADA_LINK_STEPS; ++stp) {
+				uint32_t sx[4], sz[4];
+#pragma unroll
+				for (int i = 0; i < 4; ++i) {
+					sx[i] = 0;
+					sz[i] = 1;
+					if (v[i] & RES)
+						continue;
+					const int32_t t = int32_t(v[i]) - int32_t(HISTORY_SIZE);
+					if (t < 0) {
+						if (t >= -tail_valid) {
+							sx[i] = tail[HISTORY_SIZE + t];
+							sz[i] = 0;
+						}
+					} else {
+						const int r = which(t);
+						if (r < 3) {
+							const uint64_t o = (r == 0 ? po[0] : (r == 1 ? po[1] : po[2])) +
+							                   uint64_t(t - (r == 0 ? pa[0] : (r == 1 ? pa[1] : pa[2])));
+							sx[i] = x[o];
+							sz[i] = z[o];
+						}
 					}
 				}
-			}
-			uint32_t u = 0;
 #pragma unroll
-			for (int i = 0; i < 4; ++i) {
-				if (!(v[i] & RES)) {
+				for (int i = 0; i < 4; ++i) {
+					if (v[i] & RES)
+						continue;
 					const int32_t t = int32_t(v[i]) - int32_t(HISTORY_SIZE);
 					const int r = which(t);
 					const uint32_t base = uint32_t(r == 0 ? pa[0] : (r == 1 ? pa[1] : pa[2]));
@@ -246,8 +251,11 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 					else if (t >= 0 && r < 3)
 						v[i] = base + (sx[i] | (sz[i] << 8));  // its source's own pointer
 				}
-				u += (v[i] & RES) ? 0u : 1u;
 			}
+			uint32_t u = 0;
+#pragma unroll
+			for (int i = 0; i < 4; ++i)
+				u += (v[i] & RES) ? 0u : 1u;
 			if (u) {  // the first jump round visits only the spans flagged here
 				inA |= (ab + q) / SPAN == sA;
 				inB |= (ab + q + nv - 1) / SPAN != sA;
