@@ -267,13 +267,33 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			// saves)
 			const int64_t ns = link_spans(n);
 			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
-			if (!act)
+			uint8_t* M = act ? scratch(SC_M, size_t(n) + 64) : nullptr;
+			if (!M)
 				return BULK_EXACT;
 			// init flags the spans that hold a history-derived byte: the
 			// first round reads only those
 			HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
+			// words everywhere (`full`) or only where a byte is still open
+			// after init's steps: the latter saves most of init's writes but
+			// costs the rounds a gather per word (a source's M), which only
+			// pays where few stay open.  The z decoder counts the match bytes
+			// each block reads straight from history: above 1/12 of the
+			// batch's bytes (measured: dense 0.102, mixed 0.058, chain 0),
+			// full.
+			// LZ4ADA_LINK_WORDS=full / sparse forces one.
+			int64_t hbytes = 0;
+			for (uint32_t i = 0; i < nb; ++i)
+				hbytes += stz[i].detail;
+			static const int words_env = [] {
+				const char* e = getenv("LZ4ADA_LINK_WORDS");
+				return e ? (e[0] == 'f' ? 1 : (e[0] == 's' ? 2 : 0)) : 0;
+			}();
+			const bool full = words_env ? words_env == 1 : 12 * hbytes > n;
+			if (trace)
+				fprintf(stderr, "[linked] history   %.3f of the bytes read straight from history: %s words\n",
+				        double(hbytes) / double(std::max<int64_t>(n, 1)), full ? "full" : "sparse");
 			HIP_OK(launch_link_init(bx.p, bz.p, py, ph, ny ? d_mode.p : nullptr, d_desc.p, sx.p, d_A.p, nb,
-			                        block_max, d_tail[cur].p, tail_valid, d_P.p, F, act + ns, stream));
+			                        block_max, d_tail[cur].p, tail_valid, d_P.p, F, M, act + ns, full, stream));
 			phase("init");
 			auto spans_flagged = [&](const uint8_t* a) {  // (trace only) spans a round will visit
 				if (!trace)
@@ -300,8 +320,8 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				for (int k = 0; k < 2; ++k) {
 					uint8_t* a_out = act + ((round + k) & 1) * ns;
 					const uint8_t* a_in = act + ((round + k + 1) & 1) * ns;
-					HIP_OK(launch_link_jump(d_P.p, n, d_tail[cur].p, tail_valid, F, a_in, a_out,
-					                        d_ctr.p + 2 * k, stream));
+					HIP_OK(launch_link_jump(d_P.p, M, n, d_tail[cur].p, tail_valid, F, a_in, a_out,
+					                        d_ctr.p + 2 * k, full, stream));
 					spans_flagged(a_out);
 				}
 				// the next batch's history, enqueued before the round trip (a

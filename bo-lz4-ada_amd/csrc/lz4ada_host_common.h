@@ -730,7 +730,7 @@ inline bool try_reserve(DevBuf<T>& b, size_t count)
 // 1 GiB linked frame.  lz4ada_release_device_cache() frees them.  The
 // cache is never destroyed at thread exit (the HIP runtime may be gone).
 enum ScratchRole { SC_FRAME, SC_OUT, SC_COMPACT, SC_X, SC_Y, SC_H, SC_Z, SC_TAB, SC_P, SC_F, SC_LONE, SC_U,
-	           SC_LINK, SC_N };
+	           SC_LINK, SC_M, SC_N };
 struct ScratchCache {
 	DevBuf<uint8_t> b[SC_N];
 	PinBuf pin;  // the linked path's small host transfers (pinned: no staging copy)

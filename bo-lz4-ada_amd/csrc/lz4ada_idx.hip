@@ -1427,6 +1427,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 	bool bad = false;
 	bool d1 = false;  // a match with offset >= D1_OFF reads before the block start
 	bool deep = false;  // ZL: a match reads history positions below 256
+	int32_t hcnt = 0;   // ZL: match bytes read straight from the history region
 	for (int32_t k0 = 0; k0 < nsub && !bad;) {
 		// stage input so that [k0*SUB, k0*SUB + 4 KiB) is readable
 		const int32_t cf = (k0 * SUB + mis) / BATCH;
@@ -1557,6 +1558,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 							d1 = true;
 						if (ZL && roff[r] > mdst + 65280)
 							deep = true;
+						if (ZL && roff[r] > mdst)
+							hcnt += min(rml[r], roff[r] - mdst);
 						if (mdst - roff[r] < glo)
 							anyg = true;
 					}
@@ -1801,6 +1804,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 	}
 	d1 = __any(d1);
 	deep = __any(deep);
+	if (ZL)
+		hcnt = __shfl(wave_incl_scan(hcnt), 63);
 	if (!bad && lane == 0 && (o_batch & 15))  // last partial unit
 		gstore_n(ob + (o_batch & ~15), *reinterpret_cast<const u32x4*>(&D.oring[(o_batch & ~15) & OMASK]),
 		         o_batch & 15);
@@ -1810,7 +1815,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		} else {
 			status[b].code = DS_OK;
 			status[b].aux = (d1 ? AUX_D1_RISK : 0) | (deep ? AUX_DEEP_HIST : 0);
-			status[b].detail = 0;
+			status[b].detail = ZL ? hcnt : 0;  // ZL: the linked path's density estimate
 			status[b].err_out_pos = 0;
 			status[b].out_len = uint32_t(o_batch);
 		}

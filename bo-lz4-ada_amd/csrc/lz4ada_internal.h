@@ -191,19 +191,22 @@ hipError_t side_join(hipStream_t stream);
 // Words from the planes: x (history k -> k & 255) and z (literals 0,
 // history k -> k >> 8) for every block; d_three (nullable) gives a block's
 // mode -- 1: y (~x) as well, 2: x, y and h (k >> 8) instead.
-// Each pointer is stepped once from its source's planes (d_tail: the
-// tail_valid bytes before the batch, for sources there).
+// Each pointer is stepped twice from its source's planes (d_tail: the
+// tail_valid bytes before the batch, for sources there).  d_M gets a byte
+// per position, nonzero where d_F holds the final byte already; d_P a word
+// only where it does not -- or everywhere (`full`: batches where many words
+// stay open, whose rounds then read a source's word alone).
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y, const uint8_t* h,
                             const uint8_t* d_three, const lz4ada_block_desc* d_desc,
                             const lz4ada_block_status* d_st, const int64_t* d_A, uint32_t nblocks,
                             int64_t block_max, const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_P,
-                            uint8_t* d_F, uint8_t* d_act, hipStream_t stream);
+                            uint8_t* d_F, uint8_t* d_M, uint8_t* d_act, bool full, hipStream_t stream);
 // One pointer-jumping round; d_act_in (nullptr: every span) / d_act_out:
 // a byte per span of positions, 1 while the span holds an unresolved word.
 int64_t link_spans(int64_t n);
-hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
-                            uint8_t* d_F, const uint8_t* d_act_in, uint8_t* d_act_out, uint32_t* d_ctr,
-                            hipStream_t stream);
+hipError_t launch_link_jump(uint32_t* d_P, const uint8_t* d_M, int64_t n, const uint8_t* d_tail,
+                            int64_t tail_valid, uint8_t* d_F, const uint8_t* d_act_in, uint8_t* d_act_out,
+                            uint32_t* d_ctr, bool full, hipStream_t stream);
 hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail_old,
                             uint8_t* d_tail_new, hipStream_t stream);
 

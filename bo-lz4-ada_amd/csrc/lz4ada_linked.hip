@@ -19,10 +19,10 @@
 //    byte (k - 65536) relative to its block start.  Blocks that read
 //    history positions below 256 (their high byte is 0 too) or that Z's
 //    decoder declined also take Y = ~X (and H = k >> 8): the three-plane rule;
-//  * k_link_init turns the planes into one word per output byte, a
-//    resolved byte or a pointer to an earlier position of the frame, and
-//    takes each pointer one step already: the source byte's own planes
-//    (final before init runs) say whether it is a constant;
+//  * k_link_init turns the planes into the output bytes and, for a byte
+//    that came from history, a word: a pointer to an earlier position of
+//    the frame -- taken two steps already from the source bytes' own planes
+//    (final before init runs), which resolve most of them;
 //  * k_link_jump resolves the pointers by pointer jumping (each round
 //    replaces a pointer by its target's word, so chains through many
 //    blocks finish in ~log2(length) rounds), reading positions before the
@@ -99,15 +99,17 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 // goes to F (a history-derived one as a placeholder, rewritten by the jump
 // round that resolves it), so no emit pass reads the words again.
 //
-// Each pointer is taken one step here already, from the planes of its
-// source byte (all final before this launch; the words of other blocks are
-// not: they are being written by this launch): a source in one of the
-// three blocks before b whose planes are x and z (mode 0) is a constant
-// (z = 0: its x byte) or a pointer one step further back; a source before
-// the batch is the tail's byte.  Anything else (a source further back, a
-// mode 1 / 2 block) keeps its pointer for the jump rounds.  On the bench's
-// linked frame that leaves the first round ~18% of the spans instead of
-// ~97%.
+// Each pointer is taken LZ4ADA_LINK_STEPS (2) steps here already, from the
+// planes of its source byte (all final before this launch; the words of
+// other blocks are not: they are being written by this launch): a source
+// in one of the three blocks before b whose planes are x and z (mode 0) is
+// a constant (z = 0: its x byte) or a pointer one step further back; a
+// source before the batch is the tail's byte.  Anything else (a source
+// further back, a mode 1 / 2 block) keeps its pointer for the jump rounds.
+// M gets 1 for every byte final after this, and a word is written only
+// where it is not: on the bench's linked frame (mixed) the two steps leave
+// almost nothing to the rounds, so the 4 GiB of words are never written
+// (DESIGN §7).
 constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
 #ifndef LZ4ADA_LINK_STEPS
 #define LZ4ADA_LINK_STEPS 2  // pointer steps taken in init from the planes
@@ -126,7 +128,8 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
                                                    const int64_t* __restrict__ A, uint32_t nblocks,
                                                    const uint8_t* __restrict__ tail, int32_t tail_valid,
                                                    uint32_t* __restrict__ P, uint8_t* __restrict__ F,
-                                                   uint8_t* __restrict__ act)
+                                                   uint8_t* __restrict__ M, uint8_t* __restrict__ act,
+                                                   bool full)
 {
 	// grid (parts, blocks): consecutive workgroups take consecutive parts
 	// of one block, so the waves in flight share pages of the five arrays
@@ -260,14 +263,27 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 				inA |= (ab + q) / SPAN == sA;
 				inB |= (ab + q + nv - 1) / SPAN != sA;
 			}
+			// M: 0 open (its word written), 1 final with no word written, 2
+			// final with its word written (RES | byte).  A quad's words are
+			// written when one of them is open, or every word when `full`
+			const bool wr = u != 0 || full;
+			const uint32_t mf = wr ? 2u : 1u;
 			if (nv == 4 && aligned) {
-				*reinterpret_cast<GLOBAL u32x4*>(gptr(P) + ab + q) = u32x4{ v[0], v[1], v[2], v[3] };
+				if (wr)
+					*reinterpret_cast<GLOBAL u32x4*>(gptr(P) + ab + q) = u32x4{ v[0], v[1], v[2], v[3] };
 				*reinterpret_cast<GLOBAL uint32_t*>(gptr(F) + ab + q) =
 				        (v[0] & 255u) | ((v[1] & 255u) << 8) | ((v[2] & 255u) << 16) | ((v[3] & 255u) << 24);
+				if (!full)  // (full: the rounds never read M)
+					*reinterpret_cast<GLOBAL uint32_t*>(gptr(M) + ab + q) =
+					        ((v[0] >> 31) * mf) | (((v[1] >> 31) * mf) << 8) | (((v[2] >> 31) * mf) << 16) |
+					        (((v[3] >> 31) * mf) << 24);
 			} else {
 				for (int i = 0; i < nv; ++i) {
-					P[ab + q + i] = v[i];
+					if (wr)
+						P[ab + q + i] = v[i];
 					F[ab + q + i] = uint8_t(v[i]);
+					if (!full)
+						M[ab + q + i] = uint8_t((v[i] >> 31) * mf);
 				}
 			}
 		}
@@ -294,19 +310,47 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 // the first round) instead of reading its words again.
 
 // A whole span (SPAN positions) in one wave: lane l takes positions s0 +
-// 256 j + 4 l + i (j, i < 4).  All four word loads are issued before any is
-// used, then every unresolved word's target together: four times the loads
-// in flight of round 4's quad per thread, the round's limit (a round is two
-// dependent memory trips per span).  Returns the words still unresolved.
-__device__ __forceinline__ uint32_t jump_span(GLOBAL uint32_t* Pg, int64_t s0, int64_t n,
-                                              const uint8_t* __restrict__ tail, int64_t tail_valid,
+// 256 j + 4 l + i (j, i < 4).  Its quads' M bytes first (1: final since
+// init, whose word was never written), then the words of the quads that
+// have an open position, then every open word's target together -- M, F
+// and the word of the target, selected by its M -- four times the loads in
+// flight of round 4's quad per thread.  Returns the words still unresolved.
+template <bool full>
+__device__ __forceinline__ uint32_t jump_span(GLOBAL uint32_t* Pg, const uint8_t* __restrict__ M, int64_t s0,
+                                              int64_t n, const uint8_t* __restrict__ tail, int64_t tail_valid,
                                               uint8_t* __restrict__ F, uint32_t& bad)
 {
 	const int64_t l4 = 4 * int64_t(lane_id());
+
+	uint32_t m[4];  // full: every word was written, M was not (all 0 here)
+#pragma unroll
+	for (int j = 0; j < 4; ++j) {
+		const int64_t a0 = s0 + 256 * j + l4;  // 4-aligned: spans are SPAN-aligned positions
+		if (full) {
+			m[j] = 0;
+		} else if (a0 + 4 <= n) {
+			m[j] = *reinterpret_cast<const GLOBAL uint32_t*>(gptr(M) + a0);
+		} else {
+			m[j] = 0;
+#pragma unroll
+			for (int i = 0; i < 4; ++i)
+				m[j] |= uint32_t(a0 + i < n ? M[a0 + i] : 1u) << (8 * i);
+		}
+	}
+	auto all_final = [](uint32_t q) {  // every M byte of the quad nonzero
+		return ((q & 0xffu) != 0u) & ((q & 0xff00u) != 0u) & ((q & 0xff0000u) != 0u) & ((q & 0xff000000u) != 0u);
+	};
+	if (!full && all_final(m[0]) && all_final(m[1]) && all_final(m[2]) && all_final(m[3]))
+		return 0;  // every byte final since init
 	uint32_t w[16];
 #pragma unroll
 	for (int j = 0; j < 4; ++j) {
 		const int64_t a0 = s0 + 256 * j + l4;
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			w[4 * j + i] = RES;
+		if (!full && all_final(m[j]))
+			continue;
 		if (a0 + 4 <= n) {
 			const u32x4 v = *reinterpret_cast<const GLOBAL u32x4*>(Pg + a0);
 			w[4 * j] = v.x;
@@ -318,54 +362,62 @@ __device__ __forceinline__ uint32_t jump_span(GLOBAL uint32_t* Pg, int64_t s0, i
 			for (int i = 0; i < 4; ++i)
 				w[4 * j + i] = a0 + i < n ? Pg[a0 + i] : RES;
 		}
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			if ((m[j] >> (8 * i)) & 255u)
+				w[4 * j + i] = RES;  // final since init (F has the byte)
 	}
-	uint32_t all = RES;
+	// the source's word, and (sparse words) its M beside it; its F byte
+	// only where M = 1 says the word was never written.  The M gathers
+	// double a round's time where many words stay open after init (dense:
+	// round 1 3.7 -> 6.1 ms), so such batches write every word (`full`)
+	uint32_t rs = RES;
 #pragma unroll
 	for (int k = 0; k < 16; ++k)
-		all &= w[k];
-	if (all & RES)
-		return 0;  // all resolved (their bytes are in F already)
-	uint32_t f[16];
+		rs &= w[k];
+	if (rs & RES)
+		return 0;  // all final (their bytes are in F already)
+	uint32_t f[16], mt[16];
 #pragma unroll
 	for (int k = 0; k < 16; ++k) {
 		const int64_t t = int64_t(w[k] & ~RES) - HISTORY_SIZE;
 		f[k] = w[k];
+		mt[k] = 0;
 		if (w[k] & RES)
 			continue;
-		if (t >= 0)
-			f[k] = Pg[t];  // the source's word: resolved, or a pointer further back
-		else if (t >= -tail_valid)
+		if (t >= 0) {
+			mt[k] = full ? 0u : M[t];  // full: every word was written
+			f[k] = Pg[t];
+		} else if (t >= -tail_valid) {
 			f[k] = RES | tail[HISTORY_SIZE + t];
-		else
+		} else {
 			f[k] = ~0u;  // before the frame start
+		}
 	}
+#pragma unroll
+	for (int k = 0; k < 16; ++k)
+		if (mt[k] == 1u)
+			f[k] = RES | F[int64_t(w[k] & ~RES) - HISTORY_SIZE];  // final since init, no word
 	uint32_t unres = 0;
 #pragma unroll
 	for (int j = 0; j < 4; ++j) {
 		const int64_t a0 = s0 + 256 * j + l4;
-		if ((w[4 * j] & w[4 * j + 1] & w[4 * j + 2] & w[4 * j + 3]) & RES)
-			continue;  // this quad was resolved: F has its bytes
-		uint32_t o = 0;
 #pragma unroll
 		for (int i = 0; i < 4; ++i) {
-			uint32_t& x = f[4 * j + i];
+			const int k = 4 * j + i;
+			if (w[k] & RES)
+				continue;  // final (since init or an earlier round): F has its byte
+			uint32_t x = f[k];
 			if (x == ~0u) {
 				++bad;
-				x = w[4 * j + i];
+				x = w[k];
 			}
-			if (x != w[4 * j + i])
+			if (x != w[k]) {
 				Pg[a0 + i] = x;
+				if (x & RES)
+					F[a0 + i] = uint8_t(x);
+			}
 			unres += (x & RES) ? 0u : 1u;
-			o |= (x & 255u) << (8 * i);
-		}
-		GLOBAL uint8_t* fb = gptr(F) + a0;
-		if (a0 + 4 <= n && (reinterpret_cast<uintptr_t>(fb) & 3u) == 0) {
-			*reinterpret_cast<GLOBAL uint32_t*>(fb) = o;
-		} else {
-#pragma unroll
-			for (int i = 0; i < 4; ++i)
-				if (a0 + i < n)
-					fb[i] = uint8_t(o >> (8 * i));
 		}
 	}
 	return unres;
@@ -379,8 +431,11 @@ __device__ __forceinline__ uint32_t jump_span(GLOBAL uint32_t* Pg, int64_t s0, i
 // workgroup, a __syncthreads per span).
 constexpr int32_t SPW = TPB;  // spans per workgroup pass (64 per wave)
 
-__global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int64_t n,
-                                                   const uint8_t* __restrict__ tail,
+// (one instance per word mode: `full` leaves out every M access, and the
+// registers they take: 81 VGPRs against 50, 5 waves per SIMD against 8)
+template <bool full>
+__global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, const uint8_t* __restrict__ M,
+                                                   int64_t n, const uint8_t* __restrict__ tail,
                                                    int64_t tail_valid, uint8_t* __restrict__ F,
                                                    const uint8_t* __restrict__ act_in,
                                                    uint8_t* __restrict__ act_out,
@@ -398,7 +453,7 @@ __global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, int
 			act_out[my] = 0;
 		for (uint64_t mm = __ballot(a); mm; mm &= mm - 1) {
 			const int64_t span = sb + __builtin_ctzll(mm);
-			const uint32_t u = jump_span(Pg, span * SPAN, n, tail, tail_valid, F, bad);
+			const uint32_t u = jump_span<full>(Pg, M, span * SPAN, n, tail, tail_valid, F, bad);
 			unres += u;
 			const bool any = __ballot(u != 0) != 0;
 			if (lane == 0)
@@ -438,7 +493,7 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y
                             const uint8_t* d_three, const lz4ada_block_desc* d_desc,
                             const lz4ada_block_status* d_st, const int64_t* d_A, uint32_t nblocks,
                             int64_t block_max, const uint8_t* d_tail, int64_t tail_valid, uint32_t* d_P,
-                            uint8_t* d_F, uint8_t* d_act, hipStream_t stream)
+                            uint8_t* d_F, uint8_t* d_M, uint8_t* d_act, bool full, hipStream_t stream)
 {
 	if (nblocks == 0)
 		return hipSuccess;
@@ -447,7 +502,7 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y
 	const int64_t per = 4 * 16 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
 	hipLaunchKernelGGL(link::k_link_init, dim3(gy, nblocks), dim3(link::TPB), 0, stream, x, z, y, h, d_three,
-	                   d_desc, d_st, d_A, nblocks, d_tail, int32_t(tail_valid), d_P, d_F, d_act);
+	                   d_desc, d_st, d_A, nblocks, d_tail, int32_t(tail_valid), d_P, d_F, d_M, d_act, full);
 	return hipGetLastError();
 }
 
@@ -459,14 +514,18 @@ static uint32_t grid_for(int64_t n, int64_t per_thread)
 
 int64_t link_spans(int64_t n) { return (n + link::SPAN - 1) / link::SPAN; }
 
-hipError_t launch_link_jump(uint32_t* d_P, int64_t n, const uint8_t* d_tail, int64_t tail_valid,
-                            uint8_t* d_F, const uint8_t* d_act_in, uint8_t* d_act_out, uint32_t* d_ctr,
-                            hipStream_t stream)
+hipError_t launch_link_jump(uint32_t* d_P, const uint8_t* d_M, int64_t n, const uint8_t* d_tail,
+                            int64_t tail_valid, uint8_t* d_F, const uint8_t* d_act_in, uint8_t* d_act_out,
+                            uint32_t* d_ctr, bool full, hipStream_t stream)
 {
 	if (n <= 0)
 		return hipSuccess;
-	hipLaunchKernelGGL(link::k_link_jump, dim3(grid_for(n, 4 * link::SPW)), dim3(link::TPB), 0, stream, d_P, n, d_tail,
-	                   tail_valid, d_F, d_act_in, d_act_out, d_ctr);
+	if (full)
+		hipLaunchKernelGGL(link::k_link_jump<true>, dim3(grid_for(n, 4 * link::SPW)), dim3(link::TPB), 0, stream,
+		                   d_P, d_M, n, d_tail, tail_valid, d_F, d_act_in, d_act_out, d_ctr);
+	else
+		hipLaunchKernelGGL(link::k_link_jump<false>, dim3(grid_for(n, 4 * link::SPW)), dim3(link::TPB), 0, stream,
+		                   d_P, d_M, n, d_tail, tail_valid, d_F, d_act_in, d_act_out, d_ctr);
 	return hipGetLastError();
 }
 
