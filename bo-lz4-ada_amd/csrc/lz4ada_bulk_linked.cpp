@@ -217,6 +217,9 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			HIP_OK(hipMemcpyAsync(d_mode.p, mode, nb, hipMemcpyHostToDevice, stream));
 			HIP_OK(launch_link_fill(nullptr, py, ph, d_desc.p, nb, stream));
 			std::vector<lz4ada_block_status> s_plane[2];
+			// (nb may be smaller than when sb was taken: the blocks before a
+			// failing one)
+			const size_t sbn = nb * sizeof(lz4ada_block_status);
 			for (int k = 0; k < (nh ? 2 : 1); ++k) {
 				std::vector<lz4ada_block_status> s3(stz);
 				for (uint32_t i = 0; i < nb; ++i)
@@ -224,12 +227,12 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 						s3[i].code = DS_SKIP;
 				DevBuf<lz4ada_block_status> s_dev;
 				s_dev.reserve(nb);
-				HIP_OK(hipMemcpyAsync(s_dev.p, s3.data(), sb, hipMemcpyHostToDevice, stream));
+				HIP_OK(hipMemcpyAsync(s_dev.p, s3.data(), sbn, hipMemcpyHostToDevice, stream));
 				uint8_t* buf = k == 0 ? py : ph;
 				HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, buf, s_dev.p, 2, stream));
 				HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, buf, s_dev.p, 1, LINK_HIST, stream));
 				s_plane[k].resize(nb);
-				d2h(s_plane[k].data(), s_dev.p, sb, stream);
+				d2h(s_plane[k].data(), s_dev.p, sbn, stream);
 				for (uint32_t i = 0; i < nb; ++i)
 					if (mode[i] > k &&
 					    (s_plane[k][i].code != DS_OK || s_plane[k][i].out_len != st[i].out_len))
@@ -284,10 +287,8 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			int64_t hbytes = 0;
 			for (uint32_t i = 0; i < nb; ++i)
 				hbytes += stz[i].detail;
-			static const int words_env = [] {
-				const char* e = getenv("LZ4ADA_LINK_WORDS");
-				return e ? (e[0] == 'f' ? 1 : (e[0] == 's' ? 2 : 0)) : 0;
-			}();
+			const char* we = getenv("LZ4ADA_LINK_WORDS");  // (per call: the tests force both)
+			const int words_env = we ? (we[0] == 'f' ? 1 : (we[0] == 's' ? 2 : 0)) : 0;
 			const bool full = words_env ? words_env == 1 : 12 * hbytes > n;
 			if (trace)
 				fprintf(stderr, "[linked] history   %.3f of the bytes read straight from history: %s words\n",

@@ -385,7 +385,9 @@ __device__ __forceinline__ uint32_t jump_span(GLOBAL uint32_t* Pg, const uint8_t
 		mt[k] = 0;
 		if (w[k] & RES)
 			continue;
-		if (t >= 0) {
+		if (t >= s0 + 256 * (k >> 2) + l4 + (k & 3)) {
+			f[k] = ~0u;  // never expected: every pointer goes strictly back (reported as bad)
+		} else if (t >= 0) {
 			mt[k] = full ? 0u : M[t];  // full: every word was written
 			f[k] = Pg[t];
 		} else if (t >= -tail_valid) {
