@@ -184,15 +184,19 @@ def test_linked_pointer_chains_through_every_block(batch, env):
     assert lz4ada.last_path() == lz4ada.PATH_LINKED
 
 
+@pytest.mark.parametrize("batch", [None, 300 * KiB])
 @pytest.mark.parametrize("words", ["full", "sparse"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "chain"])
-def test_linked_word_modes(kind, words, env):
+def test_linked_word_modes(kind, words, batch, env):
     """Both ways k_link_init leaves the words (lz4ada_bulk_linked.cpp picks
     one from the z decoder's history count; LZ4ADA_LINK_WORDS forces it):
-    every word, or words only where a byte is still open plus the bitmap of
-    final bytes -- whose words at ragged block starts and ends are shared
-    by two blocks (odd block lengths here), and the rounds after it."""
+    every word, or words only where a byte is still open plus the map of
+    final bytes, and the rounds after it -- over ragged block lengths, and
+    in small batches, where init's steps and the rounds read the previous
+    batch's tail for sources before the batch."""
     env("LZ4ADA_LINK_WORDS", words)
+    if batch:
+        env("LZ4ADA_LINKED_BATCH_BYTES", str(batch))
     lens = [65536, 70001, 100, 65535, 131075, 3, 65536, 200001, 4097]
     frame, raw, blocks = linked_frame(lz4ada.GEN_KINDS[kind], lens, 256 * KiB, seed=17)
     same_as_oracle(frame)
