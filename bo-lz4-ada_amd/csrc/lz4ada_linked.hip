@@ -114,6 +114,11 @@ constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
 #ifndef LZ4ADA_LINK_STEPS
 #define LZ4ADA_LINK_STEPS 2  // pointer steps taken in init from the planes
 #endif
+#ifndef LZ4ADA_LINK_LJ
+#define LZ4ADA_LINK_LJ 4  // 256-position quads per lane and wave pass (a wave takes 256 LJ positions)
+#endif
+constexpr int LJ = LZ4ADA_LINK_LJ;
+static_assert(256 * LJ <= 1024, "a wave pass meets at most two activity spans");
 #ifndef LZ4ADA_LINK_J_UNROLL
 #define LZ4ADA_LINK_J_UNROLL 1  // 0: a lane's four quads one after the other (fewer registers)
 #endif
@@ -162,16 +167,17 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 		pa[r] = more ? int32_t(A[bb]) : INT32_MAX;
 		po[r] = more ? desc[bb].out_off : 0;
 	}
-	// a wave takes 1 KiB of the block at a time, lane l its bytes g0 + 4 l +
-	// 256 j (j < 4): every load (a dword of each copy), word store (16 bytes)
+	// a wave takes 256 LJ positions of the block at a time, lane l its bytes
+	// g0 + 4 l + 256 j (j < LJ): every load (a dword of each copy), word store (16 bytes)
 	// and byte store (a dword) of the wave is one contiguous run (round 4
 	// gave each lane 16 consecutive bytes: its four 16-byte word stores were
 	// 64 bytes apart across the lanes)
-	const int64_t wave0 = 1024 * (int64_t(blockIdx.x) * (TPB / 64) + (threadIdx.x >> 6));
-	for (int64_t g0 = wave0; g0 < len; g0 += 1024 * int64_t(gridDim.x) * (TPB / 64)) {
-		uint32_t wx[4], wy[4], wh[4];
+	constexpr int64_t CH = 256 * LJ;  // positions per wave pass
+	const int64_t wave0 = CH * (int64_t(blockIdx.x) * (TPB / 64) + (threadIdx.x >> 6));
+	for (int64_t g0 = wave0; g0 < len; g0 += CH * int64_t(gridDim.x) * (TPB / 64)) {
+		uint32_t wx[LJ], wy[LJ], wh[LJ];
 #pragma unroll
-		for (int j = 0; j < 4; ++j) {
+		for (int j = 0; j < LJ; ++j) {
 			const int64_t q = g0 + 256 * j + 4 * lane;
 			wx[j] = wy[j] = wh[j] = 0;
 			if (q + 4 <= len) {
@@ -188,7 +194,7 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 					}
 			}
 		}
-		// the spans (SPAN positions each) this wave's kilobyte meets: at most two
+		// the spans (SPAN positions each) this wave pass meets: at most two
 		const int64_t sA = (ab + g0) / SPAN;
 		bool inA = false, inB = false;
 		auto which = [&](int32_t t) { return t >= pa[0] ? 0 : (t >= pa[1] ? 1 : (t >= pa[2] ? 2 : 3)); };
@@ -197,7 +203,7 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 #else
 #pragma unroll 1
 #endif
-		for (int j = 0; j < 4; ++j) {
+		for (int j = 0; j < LJ; ++j) {
 			const int64_t q = g0 + 256 * j + 4 * lane;
 			const int32_t nv = int32_t(min<int64_t>(4, max<int64_t>(len - q, 0)));
 			// words: branch-free per byte; positions fit 31 bits (bulk_linked
