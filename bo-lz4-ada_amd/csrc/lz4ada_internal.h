@@ -192,10 +192,11 @@ hipError_t side_join(hipStream_t stream);
 // history k -> k >> 8) for every block; d_three (nullable) gives a block's
 // mode -- 1: y (~x) as well, 2: x, y and h (k >> 8) instead.
 // Each pointer is stepped twice from its source's planes (d_tail: the
-// tail_valid bytes before the batch, for sources there).  d_M gets a byte
-// per position, nonzero where d_F holds the final byte already; d_P a word
-// only where it does not -- or everywhere (`full`: batches where many words
-// stay open, whose rounds then read a source's word alone).
+// tail_valid bytes before the batch, for sources there).  d_P gets a word
+// for every quad with a byte still open and d_M a byte per position (0
+// open, 1 final with no word, 2 final with its word) -- or, `full` (batches
+// where many words stay open, whose rounds then read a source's word
+// alone), every word and no d_M.
 hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y, const uint8_t* h,
                             const uint8_t* d_three, const lz4ada_block_desc* d_desc,
                             const lz4ada_block_status* d_st, const int64_t* d_A, uint32_t nblocks,

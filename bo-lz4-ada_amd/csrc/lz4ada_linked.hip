@@ -106,10 +106,12 @@ __global__ __launch_bounds__(TPB) void k_link_fill(uint8_t* __restrict__ x, uint
 // a constant (z = 0: its x byte) or a pointer one step further back; a
 // source before the batch is the tail's byte.  Anything else (a source
 // further back, a mode 1 / 2 block) keeps its pointer for the jump rounds.
-// M gets 1 for every byte final after this, and a word is written only
-// where it is not: on the bench's linked frame (mixed) the two steps leave
-// almost nothing to the rounds, so the 4 GiB of words are never written
-// (DESIGN §7).
+// Words are written only for a quad with a byte still open, and M says
+// which bytes are final (1: no word written, 2: word written) -- unless
+// `full` (a history-heavy batch, whose rounds then read words alone):
+// every word, no M.  On the bench's linked frame (mixed) the two steps
+// leave almost nothing to the rounds, so the 4 GiB of words are never
+// written.
 constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
 #ifndef LZ4ADA_LINK_STEPS
 #define LZ4ADA_LINK_STEPS 2  // pointer steps taken in init from the planes
