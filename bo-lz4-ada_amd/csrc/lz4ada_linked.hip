@@ -116,6 +116,9 @@ constexpr int64_t SPAN = 4 * TPB;  // positions per activity flag (k_link_jump)
 #ifndef LZ4ADA_LINK_STEPS
 #define LZ4ADA_LINK_STEPS 2  // pointer steps taken in init from the planes
 #endif
+#ifndef LZ4ADA_LINK_XCD
+#define LZ4ADA_LINK_XCD 1
+#endif
 #ifndef LZ4ADA_LINK_LJ
 #define LZ4ADA_LINK_LJ 4  // 256-position quads per lane and wave pass (a wave takes 256 LJ positions)
 #endif
@@ -136,13 +139,25 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
                                                    const uint8_t* __restrict__ tail, int32_t tail_valid,
                                                    uint32_t* __restrict__ P, uint8_t* __restrict__ F,
                                                    uint8_t* __restrict__ M, uint8_t* __restrict__ act,
-                                                   bool full)
+                                                   bool full, uint32_t gy)
 {
-	// grid (parts, blocks): consecutive workgroups take consecutive parts
-	// of one block, so the waves in flight share pages of the five arrays
-	const uint32_t b = blockIdx.y;
-	if (b >= nblocks)
+	// gy parts per block.  Workgroups are dealt round-robin over the 8 XCDs
+	// (MI355X_MICROARCH: blocks b and b + 8 share one), so workgroup L takes
+	// unit (L % 8) x per + L / 8 of the nblocks x gy units: each XCD runs a
+	// contiguous range of blocks in order, and a block's history sources --
+	// the previous block's last 64 KiB of both planes, read a moment before
+	// by the same XCD -- are likely still in that XCD's L2 (LZ4ADA_LINK_XCD=0
+	// at build: blocks in launch order over all XCDs, for A/B)
+	const uint32_t units = gy * nblocks;
+#if LZ4ADA_LINK_XCD
+	const uint32_t per = (units + 7) / 8;
+	const uint32_t u = (blockIdx.x % 8) * per + blockIdx.x / 8;
+#else
+	const uint32_t u = blockIdx.x;
+#endif
+	if (u >= units)
 		return;
+	const uint32_t b = u / gy, part = u % gy;
 	const uint64_t ob = desc[b].out_off;  // 256-byte aligned slot
 	const int64_t len = st[b].out_len;
 	const int64_t ab = A[b];
@@ -175,8 +190,8 @@ __global__ __launch_bounds__(TPB) void k_link_init(const uint8_t* __restrict__ x
 	// gave each lane 16 consecutive bytes: its four 16-byte word stores were
 	// 64 bytes apart across the lanes)
 	constexpr int64_t CH = 256 * LJ;  // positions per wave pass
-	const int64_t wave0 = CH * (int64_t(blockIdx.x) * (TPB / 64) + (threadIdx.x >> 6));
-	for (int64_t g0 = wave0; g0 < len; g0 += CH * int64_t(gridDim.x) * (TPB / 64)) {
+	const int64_t wave0 = CH * (int64_t(part) * (TPB / 64) + (threadIdx.x >> 6));
+	for (int64_t g0 = wave0; g0 < len; g0 += CH * int64_t(gy) * (TPB / 64)) {
 		uint32_t wx[LJ], wy[LJ], wh[LJ];
 #pragma unroll
 		for (int j = 0; j < LJ; ++j) {
@@ -455,8 +470,19 @@ __global__ __launch_bounds__(TPB) void k_link_jump(uint32_t* __restrict__ P, con
 	GLOBAL uint32_t* Pg = gptr(P);
 	const int64_t nsp = (n + SPAN - 1) / SPAN;
 	const int32_t lane = int32_t(lane_id());
-	const int64_t w0 = int64_t(blockIdx.x) * SPW + 64 * int64_t(threadIdx.x >> 6);
-	for (int64_t sb = w0; sb < nsp; sb += int64_t(gridDim.x) * SPW) {
+	// groups of SPW spans; as in k_link_init each XCD takes a contiguous
+	// range of them (workgroup L on XCD L % 8, the grid a multiple of 8), so
+	// a span's sources -- mostly in the spans just before it -- were read by
+	// the same XCD's L2
+	const int64_t ng = (nsp + SPW - 1) / SPW;
+#if LZ4ADA_LINK_XCD
+	const int64_t per = (ng + 7) / 8, g_end = min<int64_t>(ng, (blockIdx.x % 8 + 1) * per);
+	const int64_t g0 = (blockIdx.x % 8) * per + blockIdx.x / 8, gs = gridDim.x / 8;
+#else
+	const int64_t g_end = ng, g0 = blockIdx.x, gs = gridDim.x;
+#endif
+	for (int64_t g = g0; g < g_end; g += gs) {
+		const int64_t sb = g * SPW + 64 * int64_t(threadIdx.x >> 6);
 		const int64_t my = sb + lane;
 		const bool a = my < nsp && (!act_in || act_in[my]);
 		if (my < nsp && !a)
@@ -511,8 +537,10 @@ hipError_t launch_link_init(const uint8_t* x, const uint8_t* z, const uint8_t* y
 	// million 1 KiB workgroups cost more in dispatch than in work
 	const int64_t per = 4 * 16 * link::TPB;
 	const uint32_t gy = uint32_t(std::min<int64_t>(64, std::max<int64_t>(1, (block_max + per - 1) / per)));
-	hipLaunchKernelGGL(link::k_link_init, dim3(gy, nblocks), dim3(link::TPB), 0, stream, x, z, y, h, d_three,
-	                   d_desc, d_st, d_A, nblocks, d_tail, int32_t(tail_valid), d_P, d_F, d_M, d_act, full);
+	const uint32_t units = gy * nblocks;
+	const uint32_t grid = LZ4ADA_LINK_XCD ? 8 * ((units + 7) / 8) : units;
+	hipLaunchKernelGGL(link::k_link_init, dim3(grid), dim3(link::TPB), 0, stream, x, z, y, h, d_three, d_desc,
+	                   d_st, d_A, nblocks, d_tail, int32_t(tail_valid), d_P, d_F, d_M, d_act, full, gy);
 	return hipGetLastError();
 }
 
@@ -530,11 +558,12 @@ hipError_t launch_link_jump(uint32_t* d_P, const uint8_t* d_M, int64_t n, const 
 {
 	if (n <= 0)
 		return hipSuccess;
+	const uint32_t grid = (grid_for(n, 4 * link::SPW) + 7) / 8 * 8;  // (a multiple of 8: k_link_jump's XCD ranges)
 	if (full)
-		hipLaunchKernelGGL(link::k_link_jump<true>, dim3(grid_for(n, 4 * link::SPW)), dim3(link::TPB), 0, stream,
+		hipLaunchKernelGGL(link::k_link_jump<true>, dim3(grid), dim3(link::TPB), 0, stream,
 		                   d_P, d_M, n, d_tail, tail_valid, d_F, d_act_in, d_act_out, d_ctr);
 	else
-		hipLaunchKernelGGL(link::k_link_jump<false>, dim3(grid_for(n, 4 * link::SPW)), dim3(link::TPB), 0, stream,
+		hipLaunchKernelGGL(link::k_link_jump<false>, dim3(grid), dim3(link::TPB), 0, stream,
 		                   d_P, d_M, n, d_tail, tail_valid, d_F, d_act_in, d_act_out, d_ctr);
 	return hipGetLastError();
 }
