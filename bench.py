@@ -70,6 +70,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--classes", default="stored,literal,dense,rle",
                     help="extra content classes timed through the product call (N=1 only)")
+    ap.add_argument("--real", default="t1111k,liblz4_text",
+                    help="encoder-produced classes timed through the product call (N=1 only)")
     ap.add_argument("--no-linked", action="store_true",
                     help="skip the configs[4] row (1 GiB linked frame, 256 KiB blocks)")
     ap.add_argument("--no-64k", action="store_true",
@@ -300,6 +302,26 @@ def content_hash(xxhash, recs, nblocks, first=0):
     return h.intdigest()
 
 
+def host_cpu_info(threads):
+    """The host the CPU baselines ran on: CPU model, the machine's logical
+    CPUs (nproc), the CPU share this job may use and the threads used."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "threads_used": threads}
+
+
 def cpu_baseline(lz4frame, xxhash, recs, block_max, budget_s):
     """The oracle (lz4ada.adb restated in C, 'port') through the reference's
     CLI loop (tool_unlz4ada: 4 KiB reads, one Update per call), one core,
@@ -334,7 +356,7 @@ def cpu_baseline(lz4frame, xxhash, recs, block_max, budget_s):
             "kind": "port",
             "sample": f"{k} x 4 MiB blocks ({len(rawk) / MiB:.0f} MiB decoded, {dt:.1f} s) of the "
                       "same frame through the oracle's unlz4ada loop (4 KiB reads, Update per "
-                      "call, block checksums verified)"}
+                      "call, block checksums verified)", "host": host_cpu_info(1)}
 
 
 # ------------------------------------------------------------------ extra rows
@@ -376,6 +398,154 @@ def bench_class(M, dev, sh, stream, cls, nb, bmax, block_cksum=True, unique=16):
            "ratio": round(cb / rb, 4), "flg": f"0x{flg:02x}", "blocks": nb,
            "compressed_bytes": cb, "decoded_bytes": rb,
            "golden": "per-block XXH32 of the output vs the generator"}
+    del fr, de, d_out
+    return row
+
+
+# ------------------------------------------------- encoder-produced blocks
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def golden_recs(lz4ada, path, block_xxh32, raw_lens):
+    """The blocks of a committed frame as make_unique_blocks records: (record
+    bytes incl. size word [+ checksum], payload len, decoded len, decoded
+    XXH32, payload, None).  The decoded digests come with the frame (the
+    encoder's input, tests/golden/make_lz4_fixtures.py; or the frame's own
+    content checksum), not from this repo's decoder or generator."""
+    with open(path, "rb") as fh:
+        data = fh.read()
+    info, descs = lz4ada.frame_index(data)
+    recs = []
+    for i in range(info.nblocks):
+        d = descs[i]
+        has_ck = bool(d.flags & lz4ada.BLOCK_HAS_CKSUM)
+        rec = data[d.in_off - 4:d.in_off + d.in_len + (4 if has_ck else 0)]
+        recs.append((rec, d.in_len, raw_lens[i], block_xxh32[i], rec[4:4 + d.in_len], None))
+    return recs
+
+
+def real_sources(name):
+    """(recs, description) of the real-data classes:
+    t1111k -- the reference's densest test vector, one 4 MiB-BD block of
+    1,137,664 decoded bytes (test_vectors_lz4/t1111k.lz4; golden: its frame's
+    content checksum); liblz4_text -- the two 4 MiB blocks liblz4 1.9.3 made
+    of 8 MiB of seeded text (tests/golden/lz4f/big4m.lz4; golden: the
+    encoder input's per-block XXH32)."""
+    import lz4ada
+    if name == "t1111k":
+        path = os.path.join(GOLDEN, "vectors", "t1111k.lz4")
+        with open(path, "rb") as fh:
+            data = fh.read()
+        cc = int.from_bytes(data[-4:], "little")  # FLG 0x74: the content checksum ends the frame
+        return golden_recs(lz4ada, path, [cc], [1137664]), \
+            "reference vector t1111k (its one block, 222,593 sequences, ~5.1 B/sequence), tiled"
+    ent = json.load(open(os.path.join(GOLDEN, "lz4f_digests.json")))["frames"]["big4m"]
+    n = ent["input"]["len"]
+    lens = [min(4 * MiB, n - i) for i in range(0, n, 4 * MiB)]
+    return golden_recs(lz4ada, os.path.join(GOLDEN, "lz4f", "big4m.lz4"), ent["block_xxh32"], lens), \
+        "liblz4 1.9.3 (level 1) blocks of seeded text (tests/golden/lz4f/big4m.lz4), tiled"
+
+
+def match_sources(recs, hist=4080 + 16, cut_seq=128, cut_out=4080):
+    """Where the decoder's matches read from, on these blocks: HBM (more than
+    a batch + 16 bytes back, k_decode_idx's threshold), the LDS window (older
+    than the batch), or this batch's own output -- under a model of the
+    batch cut (128 sequences / 4,080 output bytes; the kernel cuts at 32-byte
+    sub-segments).  Python parse of the unique blocks, outside any timing."""
+    hbm = far = near = seqs = 0
+    offs = []
+    for rec in recs:
+        b = rec[4]
+        p, o, n = 0, 0, len(b)
+        batch_o, batch_n = 0, 0
+        while p < n:
+            t = b[p]
+            p += 1
+            L = t >> 4
+            if L == 15:
+                while True:
+                    e = b[p]
+                    p += 1
+                    L += e
+                    if e != 255:
+                        break
+            p += L
+            if p >= n:
+                break
+            off = b[p] | (b[p + 1] << 8)
+            p += 2
+            M = t & 15
+            if M == 15:
+                while True:
+                    e = b[p]
+                    p += 1
+                    M += e
+                    if e != 255:
+                        break
+            ml = M + 4
+            if batch_n >= cut_seq or o + L + ml - batch_o > cut_out:
+                batch_o, batch_n = o, 0
+            batch_n += 1
+            seqs += 1
+            m = o + L
+            if m - off < batch_o - hist:
+                hbm += 1
+            elif m - off + min(off, ml) <= batch_o:
+                far += 1
+            else:
+                near += 1
+            offs.append(off)
+            o = m + ml
+    tot = max(hbm + far + near, 1)
+    offs.sort()
+    return {"sequences": seqs, "matches": tot, "hbm_share": round(hbm / tot, 4),
+            "window_share": round(far / tot, 4), "in_batch_share": round(near / tot, 4),
+            "offset_median": offs[len(offs) // 2] if offs else 0,
+            "offset_le_64_share": round(sum(1 for x in offs if x <= 64) / tot, 4),
+            "model": "batch cut at 128 sequences / 4,080 output bytes; HBM = source more than "
+                     "4,096 bytes before the batch"}
+
+
+def bench_real(M, dev, sh, stream, name, bmax, target_bytes=8 << 30, reps=3):
+    """A real-data class through the product call (block checksums beside
+    the decode when the blocks carry them): the encoder's blocks tiled to
+    ~8 GiB of output, golden per-block XXH32 against the frame's own
+    digests."""
+    lz4ada, lz4frame, xxhash, torch = M
+    recs, what = real_sources(name)
+    per = sum(r[2] for r in recs) / len(recs)
+    nb = int(target_bytes // per)
+    fr, fl, de, eh, cb, rb, descs = assemble_shard(lz4ada, torch, recs, 0, nb, bmax, dev)
+    d_out = torch.empty(nb * bmax, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nb * 32, dtype=torch.uint8, device=dev)
+    d_hash = torch.zeros(nb, dtype=torch.int32, device=dev)
+    fp, dp, op, sp = fr.data_ptr(), de.data_ptr(), d_out.data_ptr(), d_st.data_ptr()
+    lz4ada.decode_blocks_device(fp, fl, dp, nb, op, sp, sh)
+    torch.cuda.synchronize()
+    golden_check(lz4ada, torch, d_st, descs, nb, op, dp, sp, d_hash, eh, sh, name)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        lz4ada.decode_blocks_device(fp, fl, dp, nb, op, sp, sh)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in ev) / reps
+    for a, b in ev:
+        a.record(stream)
+        lz4ada.launch_decode(fp, fl, dp, nb, op, sp, sh)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms_dec = sum(a.elapsed_time(b) for a, b in ev) / reps
+    row = {"data": what, "decode_ms": round(ms, 3), "MiB_s": round(rb / (ms * 1e-3) / MiB, 1),
+           "frac": round((cb + rb) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "decoder_alone_ms": round(ms_dec, 3),
+           "decoder_alone_frac": round((cb + rb) / (ms_dec * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "ratio": round(cb / rb, 4), "blocks": nb, "kernel": lz4ada.bulk_decoder_kernel(nb),
+           "compressed_bytes": cb, "decoded_bytes": rb,
+           "match_sources": match_sources(recs),
+           "golden": "per-block XXH32 of the output vs the frame's own digests (encoder input / "
+                     "content checksum)"}
     del fr, de, d_out
     return row
 
@@ -807,7 +977,9 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "MiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True, "scaling": "strong" if world > 1 else "weak",
+        "higher_is_better": True, "scaling": "strong",
+        "scaling_note": "N>1: configs[3]'s 32 GiB frame split over the ranks (total work fixed; "
+                        "its same-frame N=1 point is c3_one_gpu); N=1: the 8 GiB configs[2]-size frame",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic: repo LZ4 sequence generator, 64 unique blocks tiled in host memory",
         "config": {"workload": workload, "class": args.kind, "blocks_total": total_blocks,
@@ -867,6 +1039,10 @@ def main():
                 rows["stored_bcksum"] = bench_class(M, dev, sh, stream, "stored", nb, bmax)
             else:
                 rows[cls] = bench_class(M, dev, sh, stream, cls, nb, bmax)
+        for name in [c for c in args.real.split(",") if c]:
+            log(f"[bench] real-data class {name} ...")
+            torch.cuda.empty_cache()
+            rows[name] = bench_real(M, dev, sh, stream, name, bmax)
         if rows:
             result["classes"] = rows
 
@@ -889,9 +1065,13 @@ def main():
     if extra and not args.no_cpu_baseline:
         log("[bench] CPU baseline (oracle) ...")
         result["cpu_baseline"] = cpu_baseline(lz4frame, xxhash, recs, bmax, args.cpu_budget)
-        threads = min(16, os.cpu_count() or 1)
-        result["cpu_baseline_parallel"] = cpu_baseline_parallel(lz4frame, xxhash, recs, bmax,
-                                                                threads, 64)
+        # the GPU box's CPU share is 16 cores (OMP_NUM_THREADS there; nproc and
+        # os.cpu_count() show the whole machine's): one oracle thread per core
+        share = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+        threads = min(share, os.cpu_count() or 1)
+        par = cpu_baseline_parallel(lz4frame, xxhash, recs, bmax, threads, 64)
+        par["host"] = host_cpu_info(threads)
+        result["cpu_baseline_parallel"] = par
     elif rank == 0:
         result["cpu_baseline"] = None
 

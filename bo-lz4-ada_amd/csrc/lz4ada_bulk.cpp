@@ -147,7 +147,7 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const uint8_t* host_f
 		}
 		d_desc.reserve(nb);
 		d_st.reserve(nb);
-		HIP_OK(hipMemcpy(d_desc.p, d.data(), nb * sizeof(lz4ada_block_desc), hipMemcpyHostToDevice));
+		vec_h2d(d_desc, d, nullptr);
 		std::vector<lz4ada_block_status> st(nb);
 		if (!(host_frame && few_large_blocks(d) &&
 		      decode_lone_blocks(host_frame, d_frame, d, d_out, d_st.p, st,
@@ -155,8 +155,7 @@ static BulkResult bulk_independent(const uint8_t* d_frame, const uint8_t* host_f
 			HIP_OK(hipMemset(d_st.p, 0, nb * sizeof(lz4ada_block_status)));
 			HIP_OK(launch_decode_checked(d_frame, uint64_t(info.frame_len), d_desc.p, nb, d_out,
 			                             d_st.p, stream));
-			HIP_OK(hipMemcpy(st.data(), d_st.p, nb * sizeof(lz4ada_block_status),
-			                 hipMemcpyDeviceToHost));
+			vec_d2h(st, d_st, nullptr);
 		}
 		uint64_t bt_total = 0;
 		bool contiguous = true;

@@ -225,14 +225,16 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				for (uint32_t i = 0; i < nb; ++i)
 					if (mode[i] <= k)  // y: modes 1 and 2; h: mode 2
 						s3[i].code = DS_SKIP;
-				DevBuf<lz4ada_block_status> s_dev;
-				s_dev.reserve(nb);
-				HIP_OK(hipMemcpyAsync(s_dev.p, s3.data(), sbn, hipMemcpyHostToDevice, stream));
+				// the plane's statuses in plane z's half of the status scratch
+				// (free: stz is on the host), not a pooled buffer -- releasing
+				// one costs a device-wide synchronisation
+				lz4ada_block_status* const s_dev = sz.p;
+				HIP_OK(hipMemcpyAsync(s_dev, s3.data(), sbn, hipMemcpyHostToDevice, stream));
 				uint8_t* buf = k == 0 ? py : ph;
-				HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, buf, s_dev.p, 2, stream));
-				HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, buf, s_dev.p, 1, LINK_HIST, stream));
+				HIP_OK(launch_decode_idx_tab(d_frame, frame_len, d_desc.p, nb, tab.p, buf, s_dev, 2, stream));
+				HIP_OK(launch_decode_pc(d_frame, frame_len, d_desc.p, nb, buf, s_dev, 1, LINK_HIST, stream));
 				s_plane[k].resize(nb);
-				d2h(s_plane[k].data(), s_dev.p, sbn, stream);
+				d2h(s_plane[k].data(), s_dev, sbn, stream);
 				for (uint32_t i = 0; i < nb; ++i)
 					if (mode[i] > k &&
 					    (s_plane[k][i].code != DS_OK || s_plane[k][i].out_len != st[i].out_len))

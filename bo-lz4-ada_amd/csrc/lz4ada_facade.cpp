@@ -487,7 +487,7 @@ struct lz4ada_decompressor {
 	{
 		const int bcl = m.block_checksum_length;
 		const int64_t raw_len = blen - bcl;
-		if (!m.is_compressed || raw_len <= 0 || raw_len > INT32_MAX || getenv("LZ4ADA_FACADE_EXACT"))
+		if (!m.is_compressed || raw_len <= 0 || raw_len > LONE_MAX_IN || getenv("LZ4ADA_FACADE_EXACT"))
 			return false;
 		const bool linked = m.is_format == F_MODERN && !(m.flg & 0x20u);
 		const int fv = facade_variant();
@@ -688,8 +688,7 @@ struct lz4ada_decompressor {
 		ahead.d_desc.reserve(nb);
 		ahead.d_st.reserve(nb);
 		HIP_OK(hipMemcpyAsync(ahead.d_in.p, blk, size_t(pos), hipMemcpyHostToDevice, stream));
-		HIP_OK(hipMemcpyAsync(ahead.d_desc.p, ahead.descs.data(), nb * sizeof(lz4ada_block_desc),
-		                      hipMemcpyHostToDevice, stream));
+		vec_h2d(ahead.d_desc, ahead.descs, stream);
 		HIP_OK(hipMemsetAsync(ahead.d_st.p, 0, nb * sizeof(lz4ada_block_status), stream));
 		if (linked)
 			return build_ahead_linked(nb, pos, buflen);
@@ -703,9 +702,7 @@ struct lz4ada_decompressor {
 			                              stream));
 		HIP_OK(launch_decode_blocks(ahead.d_in.p, uint64_t(pos), ahead.d_desc.p, uint32_t(nb),
 		                            ahead.d_out.p, ahead.d_st.p, stream));
-		HIP_OK(hipMemcpyAsync(ahead.st.data(), ahead.d_st.p, nb * sizeof(lz4ada_block_status),
-		                      hipMemcpyDeviceToHost, stream));
-		HIP_OK(hipStreamSynchronize(stream));
+		vec_d2h(ahead.st, ahead.d_st, stream);
 		return true;
 	}
 

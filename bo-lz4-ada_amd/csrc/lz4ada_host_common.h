@@ -259,6 +259,27 @@ struct DevBuf {
 	}
 };
 
+// Per-block arrays (descriptors, statuses) between a host vector and device
+// memory, sized from the vector itself -- never from a block count captured
+// earlier (round 5: a status copy sized before a quirk-D1 stop shrank the
+// batch overran its vector) -- and checked against the device buffer's
+// capacity.
+template <class T>
+inline void vec_h2d(DevBuf<T>& d, const std::vector<T>& v, hipStream_t stream)
+{
+	if (v.size() > d.n)
+		raise(LZ4ADA_DEVICE_ERROR, "host array larger than its device buffer");
+	HIP_OK(hipMemcpyAsync(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream));
+}
+template <class T>
+inline void vec_d2h(std::vector<T>& v, const DevBuf<T>& d, hipStream_t stream)
+{
+	if (v.size() > d.n)
+		raise(LZ4ADA_DEVICE_ERROR, "host array larger than its device buffer");
+	HIP_OK(hipMemcpyAsync(v.data(), d.p, v.size() * sizeof(T), hipMemcpyDeviceToHost, stream));
+	HIP_OK(hipStreamSynchronize(stream));
+}
+
 // Pinned host memory, grow-only (the facade's output staging).
 struct PinBuf {
 	uint8_t* p = nullptr;
@@ -631,7 +652,7 @@ inline bool few_large_blocks(const std::vector<lz4ada_block_desc>& d)
 	uint32_t mx = 0;
 	for (const auto& x : d)
 		mx = std::max(mx, x.in_len);
-	return mx >= (512u << 10);
+	return mx >= (512u << 10) && int64_t(mx) <= LONE_MAX_IN;
 }
 bool decode_lone_blocks(const uint8_t* host_in, const uint8_t* d_in,
                                const std::vector<lz4ada_block_desc>& d, uint8_t* d_out,
@@ -874,6 +895,7 @@ inline void d2h(void* dst, const void* src, size_t n, hipStream_t stream)
 	HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, stream));
 	HIP_OK(hipStreamSynchronize(stream));
 }
+
 
 // Reference-exact path for one frame: the unlz4ada loop
 // (tool_unlz4ada/unlz4ada.adb:84-103) over the streaming engine, from the

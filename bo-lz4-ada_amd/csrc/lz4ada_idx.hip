@@ -170,6 +170,11 @@ __device__ __forceinline__ uint32_t fetch4(const Src& S, int32_t p)
 // select and four v_alignbyte -- ld16u's select network costs ~4x the VALU.
 __device__ __forceinline__ u32x4 ring16(const uint8_t* base, uint32_t a, uint32_t mask)
 {
+#ifdef LZ4ADA_RING16_U128  // A/B: one misaligned ds_read_b128 (callers' reads never wrap here)
+	u32x4 u;
+	__builtin_memcpy(&u, base + a, 16);
+	return u;
+#endif
 	const uint32_t a8 = a & ~7u;
 	const uint64_t q0 = *reinterpret_cast<const uint64_t*>(base + (a8 & mask));
 	const uint64_t q1 = *reinterpret_cast<const uint64_t*>(base + ((a8 + 8) & mask));
@@ -304,6 +309,7 @@ __device__ __forceinline__ bool parse_fast(const Src& S, int32_t p, int32_t n, S
 		return true;
 	return parse_seq(S, p, n, q);
 }
+
 
 // 16 bytes from global memory at byte address a, never reading at or past lim.
 __device__ __forceinline__ u32x4 gload16(uintptr_t a, uintptr_t lim)
@@ -920,7 +926,10 @@ struct alignas(16) DecLds {
 	uint8_t own[256];             // piece -> owning lane (dealt HBM pieces)
 	uint64_t rrec[4 * 64];        // pass-1 records of the staged chunks' sub-segments
 	uint64_t ldesc[2 * 64];       // literal runs of both rounds (dealt literal pieces)
+	uint32_t plut[16 * 4];        // v_perm selectors of the period-off patterns (pattern_lut_init)
+	uint8_t junk[16];             // target of the stores a lane does not need (lds_store_bf)
 };
+static_assert(sizeof(DecLds) <= 20480, "8 waves per CU: at most 20 KiB of LDS per wave");
 
 // The output window and per-wave scratch of an LDS layout: DecLds (one
 // wave per block) holds them directly; a two-wave block's view (W2, below)
@@ -929,16 +938,64 @@ __device__ __forceinline__ uint8_t* oring_of(DecLds& D) { return D.oring; }
 __device__ __forceinline__ const uint8_t* oring_of(const DecLds& D) { return D.oring; }
 __device__ __forceinline__ uint8_t* own_of(DecLds& D) { return D.own; }
 __device__ __forceinline__ uint64_t* ldesc_of(DecLds& D) { return D.ldesc; }
+// Layouts with junk bytes and the pattern selectors (the one-wave decoder):
+// branch-free exact stores (lds_store_bf) and period patterns by v_perm
+// (pattern_perm); the two-wave layouts keep the branching forms.
+template <class LD>
+struct lds_fast {
+	static constexpr bool value = false;
+};
+template <>
+struct lds_fast<DecLds> {
+	static constexpr bool value = true;
+};
+__device__ __forceinline__ uint8_t* junk_of(DecLds& D) { return D.junk; }
+__device__ __forceinline__ const uint32_t* plut_of(const DecLds& D) { return D.plut; }
+template <class LD>
+__device__ __forceinline__ uint8_t* junk_of(LD&) { return nullptr; }
+template <class LD>
+__device__ __forceinline__ const uint32_t* plut_of(const LD&) { return nullptr; }
 // the window's size - 1 (a power of two) for a layout: ORING unless the
 // layout says otherwise (the pipelined pair's 16 KiB window)
 template <class LD>
 __device__ __forceinline__ constexpr uint32_t omask_of(const LD&) { return OMASK; }
 
-// Exact-length store of n (1..16) bytes at output position x into the ring.
+// Exact store of n (0..16) bytes of v at p, without branches: each of the
+// five stores (16, 8, 4, 2, 1 bytes) goes to its place or, when n does not
+// take it, to the 16 junk bytes, so every lane runs the same five ds_write
+// instructions (lds_store_n's four divergent branches cost a wave whose
+// lanes disagree on n all of them, with their exec-mask bookkeeping).
+__device__ __forceinline__ void lds_store_bf(uint8_t* p, uint8_t* junk, u32x4 v, uint32_t n)
+{
+	const uint64_t lo = uint64_t(v.x) | (uint64_t(v.y) << 32);
+	const uint64_t hi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+	__builtin_memcpy(n >= 16u ? p : junk, &v, 16);
+	__builtin_memcpy((n & 8u) ? p : junk, &lo, 8);
+	const uint64_t r8 = (n & 8u) ? hi : lo;
+	uint8_t* const p4 = p + (n & 8u);
+	const uint32_t w4 = uint32_t(r8);
+	__builtin_memcpy((n & 4u) ? p4 : junk, &w4, 4);
+	const uint32_t r4 = (n & 4u) ? uint32_t(r8 >> 32) : w4;
+	uint8_t* const p2 = p4 + (n & 4u);
+	const uint16_t w2 = uint16_t(r4);
+	__builtin_memcpy((n & 2u) ? p2 : junk, &w2, 2);
+	*((n & 1u) ? p2 + (n & 2u) : junk) = uint8_t((n & 2u) ? (r4 >> 16) : r4);
+}
+
+// Exact-length store of n bytes (fast layouts: 0..16; else 1..16) at
+// output position x into the ring.
 template <class LD>
 __device__ __forceinline__ void ostore(LD& L, int32_t x, u32x4 v, int32_t n)
 {
 	const uint32_t a = uint32_t(x) & omask_of(L);
+	if constexpr (lds_fast<LD>::value) {
+		// a store wrapping the ring's end (one piece every 8 KiB of output)
+		// takes the byte loop below, the wave's other lanes with it
+		if (__builtin_expect(!__any(a + uint32_t(n) > omask_of(L) + 1), 1)) {
+			lds_store_bf(&oring_of(L)[a], junk_of(L), v, uint32_t(n));
+			return;
+		}
+	}
 	if (a + uint32_t(n) <= omask_of(L) + 1) {
 		// one ds_write_b128 even when misaligned: 256 cycles against 1579
 		// for four ds_write_b32 (each misaligned one is split too) and 384
@@ -1017,6 +1074,44 @@ __device__ __forceinline__ u32x4 merge_at(u32x4 a, u32x4 b, int32_t c)
 	v.z = (a.z & m(2)) | (b.z & ~m(2));
 	v.w = (a.w & m(3)) | (b.w & ~m(3));
 	return v;
+}
+
+// v_perm_b32 selectors of the period-off patterns, off = 1..15 (entry off,
+// dword d; entry 0 unused): byte t of output dword d is source byte
+// (4d + t) mod off, taken from v.y:v.x (off <= 8, and dwords 0-1 -- v.x and
+// v.y themselves -- of every off), v.z:v.x (dword 2, off >= 9) or
+// v.w:v.x / v.y:v.x (dword 3, off >= 12 / 9..11): pattern_perm.  Written
+// once per block by its wave (lane l: entry l / 4, dword l % 4).
+__device__ __forceinline__ void pattern_lut_init(uint32_t* plut)
+{
+	const uint32_t l = lane_id(), off = l >> 2, d = l & 3u;
+	uint32_t sel = 0;
+	if (off > 0)
+		for (uint32_t t = 0; t < 4; ++t) {
+			const uint32_t idx = (4 * d + t) % off;
+			uint32_t x = idx;
+			if (off > 8 && d == 2 && idx >= 8)
+				x = idx - 4;  // v.z byte idx - 8 (v_perm's src0 bytes are 4..7)
+			if (off >= 12 && d == 3 && idx >= 12)
+				x = idx - 8;  // v.w byte idx - 12
+			sel |= x << (8 * t);
+		}
+	plut[l] = sel;
+}
+
+// The phase-0 period-off (1..15) pattern of the 16 source bytes v (the
+// first off of them valid): make_pattern16's value in one LDS read, two
+// selects and four v_perm_b32 instead of its 64-bit shift network.
+__device__ __forceinline__ u32x4 pattern_perm(u32x4 v, int32_t off, const uint32_t* plut)
+{
+	const u32x4 sel = *reinterpret_cast<const u32x4*>(plut + 4 * off);
+	const uint32_t h2 = off <= 8 ? v.y : v.z, h3 = off <= 11 ? v.y : v.w;
+	u32x4 o;
+	o.x = __builtin_amdgcn_perm(v.y, v.x, sel.x);
+	o.y = __builtin_amdgcn_perm(v.y, v.x, sel.y);
+	o.z = __builtin_amdgcn_perm(h2, v.x, sel.z);
+	o.w = __builtin_amdgcn_perm(h3, v.x, sel.w);
+	return o;
 }
 
 // Match with a final source entirely inside the ring (Output_With_History,
@@ -1205,28 +1300,34 @@ __device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX
 			if (act && j1 <= j2)
 				dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
 		}
+		// the piece's reads, fixed before the steps: 16 bytes at a1 and, for
+		// an overlap with off >= 16 whose unit wraps the period, the bytes
+		// from cut on at a1 - off (one load for every form: divergent
+		// per-form loads made a step run up to three of them in turn)
+		int32_t rem = 0;
+		if (wide)
+			div_small(16 * k, ooff, rem);
+		const int32_t a1 = opat ? od - ooff : (wide ? od - ooff + rem : s_lo);
+		const int32_t cut = (wide && ooff - rem < 16) ? ooff - rem : 16;
 		bool pend = act;
 		for (;;) {
 			const uint64_t pm = __ballot(pend);
 			if (pm == 0)
 				break;
 			const bool ready = pend && (dep & pm) == 0;
-#ifdef LZ4ADA_IDX_EXP_RINGNOBODY  // timing experiment (wrong output): steps without loads/stores
-			if (ready)
-				asm volatile("" ::"v"(pd), "v"(s_lo));
-			if (false) {
-#else
-			if (ready) {
-#endif
-				// one load for every form (divergent per-form loads made a
-				// step run up to three of them one after the other)
-				int32_t rem = 0;
-				if (wide)
-					div_small(16 * k, ooff, rem);
-				const int32_t a1 = opat ? od - ooff : (wide ? od - ooff + rem : s_lo);
+			if constexpr (lds_fast<LD>::value) {
+				// every lane loads and stores (a lane not ready stores
+				// nothing: n = 0 sends its stores to the junk bytes)
 				u32x4 v = oload16(D, a1);
-				if (wide && ooff - rem < 16)
-					v = merge_at(v, oload16(D, a1 - ooff), ooff - rem);
+				if (ready && cut < 16)
+					v = merge_at(v, oload16(D, a1 - ooff), cut);
+				if (ready && opat)
+					v = pattern_perm(v, ooff, plut_of(D));
+				ostore(D, pd, v, ready ? pn : 0);
+			} else if (ready) {
+				u32x4 v = oload16(D, a1);
+				if (cut < 16)
+					v = merge_at(v, oload16(D, a1 - ooff), cut);
 				if (opat) {
 					int32_t sstp;
 					make_pattern16(uint64_t(v.x) | (uint64_t(v.y) << 32),
@@ -1387,6 +1488,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 
 	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
 	const int32_t hb = int32_t(min(hist, int64_t(65535)));  // reachable history
+	pattern_lut_init(D.plut);  // (LDS shared with pass 1: written per block)
 	if (hb > 0) {
 		// the ring's history: the previous block's last bytes
 		for (int32_t x = (-min(hb + 16, ORING - 16)) & ~15; x < 0; x += 64 * 16)
@@ -1661,9 +1763,9 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		static_assert(RMAX == 2, "literal dealing pairs two rounds");
 		{
 #pragma unroll
-			for (int r = 0; r < RMAX; ++r)
-				if (rL[r] > 0)  // rL = 0 also where a round has no sequence
-					ostore(D, rdst[r], ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, rlit[r]), min(16, rL[r]));
+			for (int r = 0; r < RMAX; ++r)  // (rL = 0 also where a round has no sequence: n = 0)
+				ostore(D, rdst[r], ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, rL[r] > 0 ? rlit[r] : S.lo),
+				       min(16, rL[r]));
 			const int32_t nc0 = rL[0] > 16 ? (rL[0] - 1) >> 4 : 0;
 			const int32_t nc1 = rL[1] > 16 ? (rL[1] - 1) >> 4 : 0;
 			if (__any(nc0 > 0 || nc1 > 0)) {
@@ -1685,9 +1787,9 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					const int32_t dst = o_batch + int32_t((dd >> 16) & 0xffffu);
 					const int32_t L = int32_t((dd >> 32) & 0xffffu);
 					const int32_t k = 1 + t - int32_t(dd >> 48);  // piece 0 went in-lane
-					if (t < tot)
-						ostore(D, dst + 16 * k, ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, lit + 16 * k),
-						       min(16, L - 16 * k));
+					const bool has = t < tot;
+					ostore(D, dst + 16 * k, ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, has ? lit + 16 * k : S.lo),
+					       has ? min(16, L - 16 * k) : 0);
 				}
 			}
 		}
@@ -1715,8 +1817,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #ifndef LZ4ADA_IDX_EXP_NOHBMST
 		// pieces of HBM-sourced matches beyond the first GC, dealt and
 		// loaded in P (the first 64 of the batch)
-		if (rpn > 0)
-			ostore(D, rpd, vr, rpn);
+		ostore(D, rpd, vr, rpn);  // (rpn = 0: none)
 #endif
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
@@ -1725,12 +1826,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
 				const bool hbm = ml > 0 && mdst - off < glo;
 #ifndef LZ4ADA_IDX_EXP_NOHBMST  // timing experiment (wrong output): no HBM-sourced stores
-				if (hbm) {
-#pragma unroll
-					for (int c = 0; c < GC; ++c)
-						if (16 * c < ml)
-							ostore(D, mdst + 16 * c, vg[r][c], min(16, ml - 16 * c));
-				}
+				static_assert(GC == 1, "one own HBM piece per match");
+				ostore(D, mdst, vg[r][0], hbm ? min(16, ml) : 0);
 #endif
 				if (rtot[r] > rfirst[r]) {  // rare: more than 64 dealt pieces; the rest now
 					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;

@@ -221,7 +221,11 @@ hipError_t launch_link_tail(const uint8_t* d_F, int64_t n, const uint8_t* d_tail
 // declines it (quirk D1); or the round's Output_Pos_History (>= 65536) --
 // the block follows a round that ended there, and quirk D1's overshoot
 // bytes are emulated (lz4ada_lone.hip).  Without history such a match
-// declines it.
+// declines it.  At most LONE_MAX_IN compressed bytes: the chain step keeps
+// every window's entry in one workgroup's registers (16 MiB of windows at
+// every window size); larger blocks return hipErrorInvalidValue, and the
+// facade sends them to the exact path instead (lone_plan).
+constexpr int64_t LONE_MAX_IN = int64_t(16) << 20;
 int64_t lone_scratch_bytes(int64_t n, int64_t cap);
 hipError_t launch_decode_lone(const uint8_t* d_blk, int64_t n, uint8_t* d_out, int64_t cap,
                               lz4ada_block_status* d_st, void* d_scratch, int64_t scratch_bytes,

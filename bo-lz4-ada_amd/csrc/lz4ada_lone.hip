@@ -517,6 +517,10 @@ __global__ __launch_bounds__(LT) void k_lone_windows(const uint8_t* __restrict__
 	// the tables of this window out (release), counted; the last window in
 	// sees every window's (acquire) and chains them
 	__shared__ uint32_t last;
+	// every thread's table stores released at agent scope before the count
+	// (the last workgroup may run on another XCD's L2; thread 0's release
+	// alone would lean on the barrier's fence being cumulative)
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 	__syncthreads();
 	if (threadIdx.x == 0)
 		last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u ==
@@ -962,6 +966,7 @@ static hipError_t lone_steps(const uint8_t* d_blk, int64_t n, int64_t cap, lz4ad
                              bool fused)
 {
 	constexpr int32_t CK = (int32_t(16) << 20) / LW / CT;
+	static_assert(int64_t(CK) * CT * LW >= LONE_MAX_IN, "the chain step covers every window");
 	const int64_t nwin = (n + LW - 1) / LW;
 	if (nwin > int64_t(CK) * CT)
 		return hipErrorInvalidValue;
@@ -1002,7 +1007,7 @@ hipError_t launch_decode_lone_parse(const uint8_t* d_blk, int64_t n, int64_t cap
                                     const uint8_t* d_h1, int32_t n1, int d1, uint8_t* d_copy, int64_t ncopy,
                                     bool fused)
 {
-	if (n <= 0 || n > (int64_t(1) << 30) || cap <= 0 || cap > (int64_t(1) << 30) ||
+	if (n <= 0 || n > LONE_MAX_IN || cap <= 0 || cap > (int64_t(1) << 30) ||
 	    scratch_bytes < lone_scratch_bytes(n, cap) || n0 < 0 || n1 < 0 || n0 + n1 > 65535 ||
 	    (d_copy && (ncopy < n || ncopy > INT32_MAX)))
 		return hipErrorInvalidValue;

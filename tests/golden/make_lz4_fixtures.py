@@ -29,6 +29,16 @@ Frames (tests/golden/lz4f/*.lz4, digests in tests/golden/lz4f_digests.json):
   d1_l20_o65535  checksum, so the output is the reference's corrupted bytes
   d1_l1_o65535   (l13_o65529 reads none of the overshoot: output == input)
   d1_cksum       the same shape with a content checksum: the reference raises
+  big4m          8 MiB of text in 4 MiB independent blocks, block checksums:
+                 tiled TILE times by the GPU tests and bench.py (independent
+                 blocks repeat freely) -- the bulk decoder's 2,048-block shape
+  big256k        8 MiB of text in 256 KiB linked blocks, block checksums: its
+                 32 blocks tiled TILE times (the first block reads no history,
+                 so every copy decodes as the first did) -- 4,096 linked blocks
+
+Each entry also lists the XXH32 of every block's decoded bytes
+("block_xxh32": the input's block-sized slices, for frames whose output is
+their input), and the tiled frames the XXH32 of their whole tiled output.
 """
 import ctypes
 import hashlib
@@ -123,6 +133,10 @@ def d1_input(seed, lit_len, off):
     return bytes(b1) + b2
 
 
+# copies of the big frames' block sequences in the tiled frames
+TILE = {"big4m": 128, "big256k": 128}
+
+
 def digest(b):
     return {"len": len(b), "sha256": hashlib.sha256(b).hexdigest(), "xxh32": xxhash.xxh32(b).intdigest()}
 
@@ -146,6 +160,8 @@ def main():
         "d1_l20_o65535": (d1_input(9, 20, 65535), dict(block=64 * KiB, linked=True, level=12)),
         "d1_l1_o65535": (d1_input(11, 1, 65535), dict(block=64 * KiB, linked=True, level=12)),
         "d1_cksum": (d1_input(10, 1, 65534), dict(block=64 * KiB, linked=True, level=12, ccksum=True)),
+        "big4m": (text(5, 8 * MiB), dict(block=4 * MiB, linked=False, bcksum=True)),
+        "big256k": (text(6, 8 * MiB), dict(block=256 * KiB, linked=True, bcksum=True)),
     }
     table = {"encoder": "liblz4 " + lib.LZ4_versionString().decode() + " (LZ4F_compressFrame, ctypes)",
              "frames": {}}
@@ -159,6 +175,15 @@ def main():
                "oracle_output": digest(out) if st == O.OK else None,
                "oracle_error": None if st == O.OK else O.exception_information(st, msg)}
         ent["output_is_input"] = st == O.OK and out == data
+        if ent["output_is_input"]:
+            blk = kw["block"]
+            ent["block_xxh32"] = [xxhash.xxh32(data[i:i + blk]).intdigest() for i in range(0, len(data), blk)]
+        if name in TILE:
+            h = xxhash.xxh32()
+            for _ in range(TILE[name]):
+                h.update(data)
+            ent["tile"] = {"copies": TILE[name], "output_len": TILE[name] * len(data),
+                           "output_xxh32": h.intdigest()}
         table["frames"][name] = ent
         print(f"{name}: {len(data)} -> {len(frame)} bytes, oracle status {st}, "
               f"output == input: {ent['output_is_input']}")

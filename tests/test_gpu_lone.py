@@ -156,3 +156,25 @@ def test_few_large_blocks_facade_read_ahead():
         if ctx.is_end_of_frame() == lz4ada.EndOfFrame.Yes:
             break
     assert bytes(out) == raw
+
+
+def test_lone_input_limit_refused_and_facade_exact():
+    """A block over LONE_MAX_IN (16 MiB compressed: the chain step holds
+    every window's entry in one workgroup) is refused by the launcher
+    instead of decoded with windows missing, and the facade
+    sends it to the exact path (Init_For_Block, lz4ada.ads:255-258): the
+    reference's bytes."""
+    comp, raw = lz4ada.gen_block(lz4ada.GEN_KINDS["literal"], 0x17, 17 << 20)
+    assert len(comp) > 16 << 20
+    with pytest.raises(lz4ada.LZ4AdaError):
+        run_lone(comp, len(raw))
+    # (the buffer holds the whole block: Min_Buffer_Size covers 8 MiB)
+    octx = O.Decompressor.init_for_block(len(comp))
+    obuf = ctypes.create_string_buffer(len(raw) + 64)
+    st, oc, of, ol = octx.update(comp, obuf)
+    assert st == O.OK and obuf.raw[of:ol + 1] == raw
+    ctx, _ = lz4ada.Decompressor.init_for_block(len(comp))
+    buf = bytearray(len(raw) + 64)
+    c, f, l = ctx.update(comp, buf)
+    assert (c, f, l) == (oc, of, ol)
+    assert bytes(buf[f:l + 1]) == raw
