@@ -751,17 +751,20 @@ def bench_facade(feed=4096, reps=5):
     import lz4frame
     exe = os.path.join(ROOT, "bo-lz4-ada_amd", "facade_bench")
     L = O.lib()
-    cases = [("indep_64k", 64 << 10, 64, True), ("linked_64k", 64 << 10, 64, False),
-             ("linked_256k", 256 << 10, 32, False), ("indep_4m", 4 << 20, 8, True)]
+    # linked_64k_d1: uniform offsets up to 65,535, so matches >= 65,529 back
+    # meet quirk D1 (lib/lz4ada.adb:811-817, 862-879) in many blocks
+    cases = [("indep_64k", 64 << 10, 64, True, "mixed"), ("linked_64k", 64 << 10, 64, False, "mixed_nod1"),
+             ("linked_64k_d1", 64 << 10, 64, False, "mixed"),
+             ("linked_256k", 256 << 10, 32, False, "mixed_nod1"), ("indep_4m", 4 << 20, 8, True, "mixed")]
     rows = {}
     with tempfile.TemporaryDirectory() as td:
-        for name, bmax, nb, indep in cases:
+        for name, bmax, nb, indep, kind in cases:
             if indep:
-                blocks = [(*lz4ada.gen_block(lz4ada.GEN_KINDS["mixed"], SEED0 + i, bmax), False)
+                blocks = [(*lz4ada.gen_block(lz4ada.GEN_KINDS[kind], SEED0 + i, bmax), False)
                           for i in range(nb)]
-            else:  # offsets below 65529: no block meets quirk D1
+            else:  # mixed_nod1: offsets below 65529, no block meets quirk D1
                 blocks = [(c, r, False) for c, r in
-                          lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS["mixed_nod1"], SEED0, bmax, nb)]
+                          lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS[kind], SEED0, bmax, nb)]
             frame, _ = lz4frame.build_frame(blocks, bmax, indep=indep, block_cksum=True,
                                             content_cksum=True)
             st, expect, msg = O.unlz4ada(frame, out_cap=len(frame) * 4 + (8 << 20))
@@ -788,13 +791,41 @@ def bench_facade(feed=4096, reps=5):
                 assert st == O.OK and n.value == len(expect)
                 best = dt if best is None else min(best, dt)
             row["oracle_1core_mib_s"] = round(len(expect) / best / MiB, 1)
-            row["frame"] = (f"{nb} x {bmax >> 10} KiB {'independent' if indep else 'linked'} mixed "
+            row["frame"] = (f"{nb} x {bmax >> 10} KiB {'independent' if indep else 'linked'} {kind} "
                             f"blocks, block + content checksum, {len(expect) / MiB:.0f} MiB decoded")
             rows[name] = row
+    rows["bulk_linked_64k_d1"] = bench_d1_frame()
     rows["note"] = (f"bo-lz4-ada_amd/facade_bench: {feed}-byte Update calls from C, median of {reps} "
                     "frames, a context per frame, output checked; oracle_1core_mib_s: the oracle's "
                     "unlz4ada loop over the same frame (1 core)")
     return rows
+
+
+def bench_d1_frame(nb=256, reps=5):
+    """256 linked 64 KiB blocks with uniform offsets
+    (quirk D1 in many blocks) through lz4ada_decode_frame from host memory,
+    output equal to the oracle's (the reference's bytes, D1 included);
+    median of `reps`, and which paths ran (lz4ada_last_path)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    import lz4ada
+    import lz4frame
+    blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS["mixed"], 0x4C5A3441, 64 << 10, nb)
+    frame, _ = lz4frame.build_frame([(c, r, False) for c, r in blocks], 64 << 10, indep=False)
+    st, ref, msg = O.unlz4ada(frame, out_cap=nb * (64 << 10) + (1 << 20))
+    assert st == O.OK, msg
+    lz4ada.decode_frame(frame)  # warm
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out, used = lz4ada.decode_frame(frame)
+        ts.append(time.perf_counter() - t0)
+        assert out == ref and used == len(frame)
+    ts.sort()
+    t = ts[len(ts) // 2]
+    return {"ms": round(t * 1e3, 2), "mib_s": round(len(ref) / t / MiB, 1), "path": lz4ada.last_path(),
+            "frame": f"{nb} x 64 KiB linked mixed blocks (uniform offsets), no checksums, host in/out",
+            "note": "lz4ada_decode_frame, median of %d; path bits: 2 linked bulk, 4 exact resume" % reps}
 
 
 # ----------------------------------------------------------------------- main

@@ -338,6 +338,10 @@ static void decode_one_frame(const uint8_t* f, int64_t len, Sink& out, int64_t& 
 				phase("resume");
 				return;
 			}
+			if (trace)
+				fprintf(stderr, "[frame] bulk result %d fail %lld total %llu hash %08x declared %08x\n", int(r),
+				        (long long)fail, (unsigned long long)total, h ? (total ? hs.hash : 0x02cc5d05u) : 0u,
+				        h ? info.content_checksum_declared : 0u);
 			if (r == BULK_OK && (!info.has_content_size || total == info.content_size) &&
 			    (!h || (total == 0 ? 0x02cc5d05u : hs.hash) == info.content_checksum_declared)) {
 				consumed = info.frame_len;

@@ -41,6 +41,11 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		        std::chrono::duration<double, std::milli>(t1 - t0).count());
 		t0 = t1;
 	};
+	auto why = [&](BulkResult r, const char* reason) {  // (trace) why the batch loop ends
+		if (trace)
+			fprintf(stderr, "[linked] result %d: %s\n", int(r), reason);
+		return r;
+	};
 	// the small per-call buffers -- both history tails, and per batch the
 	// descriptors, both planes' statuses, A, the modes and the round counters
 	// -- carved from one thread-cached device buffer, and their host sides
@@ -53,7 +58,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 	             o_ctr = o_mode + al(nmax), link_bytes = o_ctr + 256;
 	uint8_t* const lk = scratch(SC_LINK, link_bytes);
 	if (!lk)
-		return BULK_EXACT;
+		return why(BULK_EXACT, "exit at line 61");
 	PinBuf& pin = scratch_cache().pin;
 	pin.reserve(link_bytes);
 	uint8_t* const hp = pin.p;  // host twin of lk: hp + o is the host side of lk + o
@@ -92,6 +97,24 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			x.out_off = bytes + uint64_t(HISTORY_SIZE);
 			bytes += uint64_t(HISTORY_SIZE) + round256(x.out_cap);
 		}
+		// quirk D1's round state, predicted with every block filling its
+		// slot (Output_Pos / Output_Pos_History, lz4ada.adb:678-690,
+		// 785-787): the index decoder emulates D1 under it, and the replay
+		// below accepts a block only if the real state is the predicted one
+		{
+			int64_t po = opos, ph = oph;
+			for (auto& x : d) {
+				if (po >= HISTORY_SIZE)
+					po = 0;
+				x.flags &= LZ4ADA_BLOCK_STORED | LZ4ADA_BLOCK_HAS_CKSUM;
+				if (ph >= HISTORY_SIZE && ph <= HISTORY_SIZE + 6)
+					x.flags |= BLOCK_D1_ROUND | (uint32_t(ph - HISTORY_SIZE) << BLOCK_D1_OPH_SHIFT) |
+					           (uint32_t(po) << BLOCK_N1_SHIFT);
+				po += int64_t(x.out_cap);
+				if (po >= HISTORY_SIZE)
+					ph = po;
+			}
+		}
 		// two planes for every block (x: history k -> k & 255; z: literals
 		// as zeros, history k -> k >> 8), two more (y, h) only for the blocks
 		// z cannot serve
@@ -104,7 +127,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				budget /= 2;
 				continue;
 			}
-			return BULK_EXACT;
+			return why(BULK_EXACT, "exit at line 130");
 		}
 		// planes x's and z's statuses side by side: one copy back
 		struct {
@@ -158,9 +181,27 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		for (uint32_t i = 0; i < nb; ++i) {
 			if (opos >= HISTORY_SIZE)
 				opos = 0;
+			// quirk D1: a block with a match >= D1_OFF back before its start
+			// (AUX_D1_RISK) in a round after one that ended at 65536..65542
+			// is the decoders' only if the index decoder (which emulates D1)
+			// decoded it under the real round state; one decoded under a D1
+			// prediction the real state does not have goes too (without
+			// such a match, neither the quirk nor the emulation changes a byte)
+			const bool in_d1 = oph >= HISTORY_SIZE && oph <= HISTORY_SIZE + 6;
+			const bool emu = (st[i].aux & AUX_D1_EMU) != 0;
+			// (plane z declined: planes y and h come from k_decode_pc, which
+			// does not emulate D1 -- the planes would disagree)
+			const bool pred_ok = emu && in_d1 && (d[i].flags & BLOCK_D1_ROUND) && stz[i].code == DS_OK &&
+			                     int64_t((d[i].flags >> BLOCK_D1_OPH_SHIFT) & 7u) == oph - HISTORY_SIZE &&
+			                     int64_t(d[i].flags >> BLOCK_N1_SHIFT) == opos;
+			const bool d1_bad = (st[i].aux & AUX_D1_RISK) && (in_d1 ? !pred_ok : emu);
+			if (trace > 2)
+				fprintf(stderr, "[linked] block %u: code %d aux %d len %u z %d | opos %lld oph %lld pred %s%u/%u%s\n",
+				        lo + i, st[i].code, st[i].aux, st[i].out_len, stz[i].code, (long long)opos, (long long)oph,
+				        (d[i].flags & BLOCK_D1_ROUND) ? "" : "-", (d[i].flags >> BLOCK_D1_OPH_SHIFT) & 7u,
+				        d[i].flags >> BLOCK_N1_SHIFT, d1_bad ? " D1 STOP" : "");
 			if (st[i].code != DS_OK ||
-			    ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum) ||
-			    ((st[i].aux & AUX_D1_RISK) && oph >= HISTORY_SIZE && oph <= HISTORY_SIZE + 6)) {
+			    ((d[i].flags & LZ4ADA_BLOCK_HAS_CKSUM) && st[i].cksum != d[i].cksum) || d1_bad) {
 				ok_n = i;
 				break;
 			}
@@ -174,7 +215,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			fail = int64_t(lo) + ok_n;
 			nb = ok_n;
 			if (nb == 0)
-				return BULK_FAIL_AT;
+				return why(BULK_FAIL_AT, "fail-at exit at line 211");
 		}
 		if (n >= (int64_t(1) << 31) - HISTORY_SIZE) {  // words hold positions + 65536 in 31 bits
 			if (nb > 1) {
@@ -186,7 +227,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				oph = oph0;
 				continue;
 			}
-			return BULK_EXACT;
+			return why(BULK_EXACT, "exit at line 223");
 		}
 		// blocks plane z cannot serve alone: one that reads history positions
 		// below 256 (AUX_DEEP_HIST: their high byte is 0, like a literal's)
@@ -213,7 +254,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			py = scratch(SC_Y, size_t(bytes));
 			ph = py && nh ? scratch(SC_H, size_t(bytes)) : nullptr;
 			if (!py || (nh && !ph))
-				return BULK_EXACT;
+				return why(BULK_EXACT, "exit at line 250");
 			HIP_OK(hipMemcpyAsync(d_mode.p, mode, nb, hipMemcpyHostToDevice, stream));
 			HIP_OK(launch_link_fill(nullptr, py, ph, d_desc.p, nb, stream));
 			std::vector<lz4ada_block_status> s_plane[2];
@@ -238,7 +279,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				for (uint32_t i = 0; i < nb; ++i)
 					if (mode[i] > k &&
 					    (s_plane[k][i].code != DS_OK || s_plane[k][i].out_len != st[i].out_len))
-						return BULK_EXACT;  // never expected: plane x decoded it
+						return why(BULK_EXACT, "never expected: plane x decoded it");
 			}
 			phase("more planes");
 		}
@@ -252,7 +293,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			uint32_t* p;
 		} d_P{ reinterpret_cast<uint32_t*>(scratch(SC_P, size_t(std::max<int64_t>(n, 1)) * 4)) };
 		if (!d_P.p)
-			return BULK_EXACT;
+			return why(BULK_EXACT, "exit at line 289");
 		HIP_OK(hipMemcpyAsync(d_A.p, A, nb * sizeof(int64_t), hipMemcpyHostToDevice, stream));
 		const int64_t tail_valid = std::min<int64_t>(int64_t(total) + hist0, HISTORY_SIZE);
 		uint8_t* F = nullptr;
@@ -264,7 +305,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			// bytes it resolves: the last round leaves the output
 			F = sink.dst(n);
 			if (!F)
-				return BULK_EXACT;
+				return why(BULK_EXACT, "exit at line 301");
 			// span activity flags, double-buffered across rounds (an init that
 			// also stepped every history-derived byte one pointer forward was
 			// measured and dropped: mixed 10.32 vs 10.35 ms, chain 13.5 vs
@@ -274,7 +315,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			uint8_t* act = scratch(SC_U, size_t(2 * ns + 64));
 			uint8_t* M = act ? scratch(SC_M, size_t(n) + 64) : nullptr;
 			if (!M)
-				return BULK_EXACT;
+				return why(BULK_EXACT, "exit at line 311");
 			// init flags the spans that hold a history-derived byte: the
 			// first round reads only those
 			HIP_OK(hipMemsetAsync(act + ns, 0, size_t(ns), stream));
@@ -318,7 +359,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 			uint32_t left = 1;
 			for (int round = 0; left > 0; round += 2) {
 				if (round > 64)
-					return BULK_EXACT;  // never expected: every pointer goes strictly back
+					return why(BULK_EXACT, "never expected: every pointer goes strictly back");
 				HIP_OK(hipMemsetAsync(d_ctr.p, 0, 4 * sizeof(uint32_t), stream));
 				for (int k = 0; k < 2; ++k) {
 					uint8_t* a_out = act + ((round + k) & 1) * ns;
@@ -333,7 +374,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 				uint32_t* c4 = reinterpret_cast<uint32_t*>(hp + o_ctr);
 				d2h(c4, d_ctr.p, 4 * sizeof(uint32_t), stream);
 				if (c4[1] || c4[3])
-					return BULK_EXACT;  // a reference before the frame start: the exact error
+					return why(BULK_EXACT, "a reference before the frame start: the exact error");
 				left = c4[2];  // words still unresolved after the pair's second round
 			}
 			phase("jumps");
@@ -346,7 +387,7 @@ BulkResult bulk_linked(const uint8_t* d_frame, uint64_t frame_len, int64_t block
 		for (uint32_t i = 0; i < nb; ++i)
 			lens.push_back(st[i].out_len);
 		if (fail >= 0)
-			return BULK_FAIL_AT;
+			return why(BULK_FAIL_AT, "fail-at exit at line 383");
 		lo = hi;
 	}
 	return BULK_OK;

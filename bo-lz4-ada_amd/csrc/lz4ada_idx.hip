@@ -170,11 +170,6 @@ __device__ __forceinline__ uint32_t fetch4(const Src& S, int32_t p)
 // select and four v_alignbyte -- ld16u's select network costs ~4x the VALU.
 __device__ __forceinline__ u32x4 ring16(const uint8_t* base, uint32_t a, uint32_t mask)
 {
-#ifdef LZ4ADA_RING16_U128  // A/B: one misaligned ds_read_b128 (callers' reads never wrap here)
-	u32x4 u;
-	__builtin_memcpy(&u, base + a, 16);
-	return u;
-#endif
 	const uint32_t a8 = a & ~7u;
 	const uint64_t q0 = *reinterpret_cast<const uint64_t*>(base + (a8 & mask));
 	const uint64_t q1 = *reinterpret_cast<const uint64_t*>(base + ((a8 + 8) & mask));
@@ -842,6 +837,8 @@ __device__ __forceinline__ bool batch_global(const Src& S, g8* ob, uintptr_t oli
 			if (q.ml > 0) {
 				if (q.off > mdst + hb)
 					pre = true;  // reference before the block start (D2)
+				if (hb > 0 && q.off > mdst && q.off >= D1_OFF)
+					pre = true;  // a possible quirk-D1 read: P flags / emulates those, so decline
 				const int32_t dep_end = mdst - q.off + min(q.off, q.ml);
 				if (q.ml > LONG || dep_end > o_batch) {
 					if (!has) {
@@ -1076,6 +1073,12 @@ __device__ __forceinline__ u32x4 merge_at(u32x4 a, u32x4 b, int32_t c)
 	return v;
 }
 
+// Store step of a period-off pattern match (make_pattern16's stp).
+__device__ __forceinline__ int32_t pattern_step(int32_t off)
+{
+	return off <= 8 ? int32_t((PAT_LUT >> (5 * (off - 1))) & 31u) : off;
+}
+
 // v_perm_b32 selectors of the period-off patterns, off = 1..15 (entry off,
 // dword d; entry 0 unused): byte t of output dword d is source byte
 // (4d + t) mod off, taken from v.y:v.x (off <= 8, and dwords 0-1 -- v.x and
@@ -1128,9 +1131,15 @@ __device__ __forceinline__ void ring_match(LD& L, int32_t dst, int32_t off, int3
 	u32x4 pv = oload16(L, src);
 	int32_t stp = 16;
 	const bool pat = off < 16 && off < len;
-	if (pat)
-		make_pattern16(uint64_t(pv.x) | (uint64_t(pv.y) << 32), uint64_t(pv.z) | (uint64_t(pv.w) << 32),
-		               off, pv, stp);
+	if (pat) {
+		if constexpr (lds_fast<LD>::value) {
+			pv = pattern_perm(pv, off, plut_of(L));
+			stp = pattern_step(off);
+		} else {
+			make_pattern16(uint64_t(pv.x) | (uint64_t(pv.y) << 32), uint64_t(pv.z) | (uint64_t(pv.w) << 32),
+			               off, pv, stp);
+		}
+	}
 	ostore(L, dst, pv, min(16, len));
 	int32_t start = 0;  // unit x of the wide form begins at source byte x mod off
 	for (int32_t x = stp; x < len; x += stp) {
@@ -1164,11 +1173,6 @@ __device__ __forceinline__ int32_t div_small(int32_t t, int32_t d, int32_t& r)
 	return q;
 }
 
-// Store step of a period-off pattern match (make_pattern16's stp).
-__device__ __forceinline__ int32_t pattern_step(int32_t off)
-{
-	return off <= 8 ? int32_t((PAT_LUT >> (5 * (off - 1))) & 31u) : off;
-}
 
 __device__ __forceinline__ int32_t piece_owner(int32_t inc, int32_t t);
 
@@ -1234,13 +1238,25 @@ __device__ __forceinline__ int32_t match_pieces(int32_t off, int32_t ml)
 	return stp == 16 ? (ml + 15) >> 4 : div_small(ml + stp - 1, stp, rr);
 }
 
+#ifndef LZ4ADA_FWD_ROUNDS
+#define LZ4ADA_FWD_ROUNDS 5
+#endif
+constexpr int FWD_ROUNDS = LZ4ADA_FWD_ROUNDS;  // forwarding rounds of ring_lanes (0: none)
+// ... and of ring_pieces: off (mixed 13.17 -> 13.41 ms with it, dense
+// 37.07 -> 37.38: its dealt pieces rarely sit inside one producer piece,
+// and the set-up runs for every 64-piece chunk; profiles/r06i_ab.txt)
+#ifndef LZ4ADA_FWD_PIECES
+#define LZ4ADA_FWD_PIECES 0
+#endif
+constexpr int FWD_PIECES = LZ4ADA_FWD_PIECES;
+
 // Both rounds' ring-sourced matches (round r: mdst[r], off[r], ml[r]; ml 0:
 // none), dealt together in output order; a piece finds its match in an LDS
 // descriptor (D.ldesc, free after the literals) instead of by shuffles.
 template <class LD>
 __device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX],
                                                const int32_t (&off)[RMAX], const int32_t (&ml)[RMAX],
-                                               int32_t o_batch)
+                                               int32_t o_batch, int32_t glo = INT32_MIN)
 {
 	int32_t steps = 0;  // store steps (diagnostic count)
 	const int32_t lane = int32_t(lane_id());
@@ -1259,11 +1275,7 @@ __device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX
 	for (int32_t t0 = 0; t0 < tot; t0 += 64) {
 		const int32_t t = t0 + lane;
 		const bool act = t < tot;
-#ifdef LZ4ADA_IDX_EXP_NOOWNER  // timing experiment (wrong output): no owner search
-		const int32_t lo = lane;
-#else
 		const int32_t lo = min(chunk_owner2(D, inc0, np0, inc1, np1, t0), 127);
-#endif
 		const uint64_t dd = ldesc[lo];
 		const int32_t od = o_batch + int32_t(dd & 0xffffu);
 		const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
@@ -1282,12 +1294,8 @@ __device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX
 		// a piece writes [pd, pd + pn): its end, not pd + 16 (a short last piece
 		// must not hold back a source that only starts after it)
 		const int32_t pe = act ? pd + pn : INT32_MAX, ps = act ? pd : INT32_MAX;
-		uint64_t dep = 0;
-#ifdef LZ4ADA_IDX_EXP_NODEP  // timing experiment (wrong output): no dependency order
-		if (false) {
-#else
+		int32_t fj1 = 64, fj2 = -1;  // the chunk's pieces that write this one's source (none)
 		if (!__all(!act || s_hi <= __shfl(ps, 0))) {
-#endif
 			int32_t j1 = 0, c2 = 0;
 #pragma unroll
 			for (int st = 32; st >= 1; st >>= 1) {
@@ -1296,10 +1304,39 @@ __device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX
 				if (__shfl(ps, c2 + st - 1) < s_hi)
 					c2 += st;
 			}
-			const int32_t j2 = min(c2 - 1, lane - 1);
-			if (act && j1 <= j2)
-				dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
+			fj1 = j1;
+			fj2 = min(c2 - 1, lane - 1);
 		}
+		// Forwarding (ring_lanes' pointer jumping, per piece): a piece whose
+		// source [s_lo, s_hi) lies inside ONE earlier piece P of the chunk, P
+		// a plain copy (out[y] = out[y - sh_P] over its bytes, sh_P = its
+		// offset plus its own forwarding), reads F bytes further back
+		// instead and waits for P's producers; every read form shifts as a
+		// whole (a pattern's period, an overlap's two reads)
+		int32_t F = 0;
+		if (FWD_PIECES > 0 && glo != INT32_MIN) {
+			const bool plain = act && !opat && !wide;
+			int32_t sh = ooff;
+			const int32_t q0 = __shfl(ps, fj1), qe = __shfl(pe, fj1);
+			bool fw = act && fj1 == fj2 && q0 <= s_lo && s_hi <= qe && __shfl(int32_t(plain), fj1) != 0;
+			for (int r = 0; r < FWD_PIECES && __any(fw); ++r) {
+				const int32_t p = fj1;
+				const int32_t qs = __shfl(sh, p), q1 = __shfl(fj1, p), q2 = __shfl(fj2, p);
+				const bool qf = __shfl(int32_t(fw), p) != 0;
+				if (fw && s_lo - F - qs >= glo) {
+					F += qs;
+					sh = ooff + F;
+					fj1 = q1;  // P's producers (none: q1 > q2, the source is final)
+					fj2 = q2;
+					fw = qf;
+				} else {
+					fw = false;
+				}
+			}
+		}
+		uint64_t dep = 0;
+		if (act && fj1 <= fj2)
+			dep = (fj2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << fj2) - 1)) & ~((uint64_t(1) << fj1) - 1);
 		// the piece's reads, fixed before the steps: 16 bytes at a1 and, for
 		// an overlap with off >= 16 whose unit wraps the period, the bytes
 		// from cut on at a1 - off (one load for every form: divergent
@@ -1307,7 +1344,7 @@ __device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX
 		int32_t rem = 0;
 		if (wide)
 			div_small(16 * k, ooff, rem);
-		const int32_t a1 = opat ? od - ooff : (wide ? od - ooff + rem : s_lo);
+		const int32_t a1 = (opat ? od - ooff : (wide ? od - ooff + rem : s_lo)) - F;
 		const int32_t cut = (wide && ooff - rem < 16) ? ooff - rem : 16;
 		bool pend = act;
 		for (;;) {
@@ -1356,19 +1393,23 @@ __device__ __forceinline__ int32_t ring_pieces(LD& D, const int32_t (&mdst)[RMAX
 constexpr int RING_LANE_MAX = LZ4ADA_RING_LANE_MAX;
 template <class LD>
 __device__ __forceinline__ int32_t ring_lanes(LD& D, int32_t mdst, int32_t off, int32_t ml,
-                                           int32_t rbeg, int32_t L)
+                                           int32_t rbeg, int32_t L, int32_t glo = INT32_MIN)
 {
 	const int32_t lane = int32_t(lane_id());
 	const int32_t src = mdst - off;
 	const int32_t dep_end = src + min(off, ml);
 	const bool far = ml > 0 && (dep_end <= rbeg || off <= L);
-	bool near = ml > 0 && !far;
-	int32_t steps = 0;  // near-match steps (diagnostic count)
-	if (far)
-		ring_match(D, mdst, off, ml);
-	wave_lds_fence();
-	if (!__any(near))
+	int32_t steps = 0;  // store steps (diagnostic count)
+	if (!__any(ml > 0 && !far)) {
+		if (far)
+			ring_match(D, mdst, off, ml);
+		wave_lds_fence();
 		return 0;
+	}
+	// with near matches, the far ones run in the first step with the near
+	// ones that are ready (their sources are final: no producers), not in
+	// a step of their own
+	bool near = ml > 0;
 	const int32_t mend = mdst + ml;
 	int32_t j1 = 0, c2 = 0;
 #pragma unroll
@@ -1378,17 +1419,49 @@ __device__ __forceinline__ int32_t ring_lanes(LD& D, int32_t mdst, int32_t off, 
 		if (__shfl(mdst, c2 + st - 1) < dep_end)
 			c2 += st;
 	}
-	const int32_t j2 = min(c2 - 1, lane - 1);
+	int32_t fj1 = far ? 64 : j1, fj2 = far ? -1 : min(c2 - 1, lane - 1);
+	// Forwarding (pointer jumping over the round's near matches): a plain
+	// match (off >= ml) whose source lies inside ONE earlier near match P of
+	// the round, P itself a plain copy, reads P's source instead -- byte x of
+	// it is byte x - off - off_P -- and waits for P's producers instead of
+	// for P.  Each round composes every lane's forwarding with its producer's
+	// current one, so a chain of k dependent matches (text: matches copying
+	// recent matches, ~17 in a row) takes ~log2 k rounds instead of k store
+	// steps.  A source forwarded past glo (below the window's kept bytes)
+	// stops there.
+	int32_t fo = off;
+	{
+		const int32_t pm = __shfl(mdst, fj1), pe = __shfl(mend, fj1), po = __shfl(off, fj1);
+		const bool pn = __shfl(int32_t(near), fj1) != 0;
+		bool fw = FWD_ROUNDS > 0 && glo != INT32_MIN && near && off >= ml && fj1 == fj2 && pm <= src &&
+		          dep_end <= pe && pn && po >= pe - pm;
+		// (the producer's state is read before any lane updates its own:
+		// synchronous rounds; P's identity out[y] = out[y - fo_P] holds for
+		// whatever forwarding P has reached)
+		for (int r = 0; r < FWD_ROUNDS && __any(fw); ++r) {
+			const int32_t p = fj1;
+			const int32_t qo = __shfl(fo, p), q1 = __shfl(fj1, p), q2 = __shfl(fj2, p);
+			const bool qf = __shfl(int32_t(fw), p) != 0;
+			if (fw && mdst - fo - qo >= glo) {
+				fo += qo;
+				fj1 = q1;  // P's producers (none: q1 > q2, the source is final)
+				fj2 = q2;
+				fw = qf;
+			} else {
+				fw = false;
+			}
+		}
+	}
 	uint64_t dep = 0;
-	if (near && j1 <= j2)
-		dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
+	if (near && fj1 <= fj2)
+		dep = (fj2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << fj2) - 1)) & ~((uint64_t(1) << fj1) - 1);
 	for (;;) {
 		const uint64_t pending = __ballot(near);
 		if (pending == 0)
 			break;
 		const bool ready = near && (dep & pending) == 0;
 		if (ready) {
-			ring_match(D, mdst, off, ml);
+			ring_match(D, mdst, fo, ml);
 			near = false;
 		}
 		wave_lds_fence();
@@ -1423,6 +1496,48 @@ __device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_
 	}
 }
 
+// Quirk D1 under the host's predicted round state (BLOCK_D1_ROUND: the
+// last round ended at OPH in [65536, 65542] and this block starts at round
+// position n1).  A match reading before the round start within 7 bytes of
+// where that round ended (OPH - off < 8) reads what the reference's last
+// wild copy (lib/lz4ada.adb:811-817) left past its frontier, not history:
+// * after literals (L > 0): the payload bytes after them -- emulated when
+//   their last chunk was wild (8 payload bytes left, k_lone_words' rule);
+// * with no literals: the previous match's last Write_Output call
+//   (:845-904), i.e. the output bytes right after that match's source --
+//   emulated when the match was one call (no repeating part; from history,
+//   no intermediate part either) whose tail read only final bytes (in the
+//   round: its source ends pad bytes before its output; from history: the
+//   tail stays in the previous round, and that match is no D1 read
+//   itself).  `lit` then carries that position (block-relative, + D1_QBIAS,
+//   << 3) and the overshoot length pad (low 3 bits) for M.
+// Either way the match must read nothing of the current round.  false: a
+// D1 read it does not emulate (the block is declined).  The rule was
+// checked against the oracle's output over 256-block linked frames of the
+// generator's uniform-offset kinds (tools/d1_model.py).
+constexpr int32_t D1_QBIAS = 1 << 17;
+__device__ __forceinline__ bool d1_emulable(int32_t mdst, int32_t L, int32_t& lit, int32_t off, int32_t ml,
+                                            int32_t pmd, int32_t pof, int32_t pml, int32_t n1, int32_t oph,
+                                            int32_t n, int32_t glo)
+{
+	if (!(n1 + mdst < off && oph - off < 8))
+		return true;  // no D1 read
+	if (n1 + mdst + ml > off)
+		return false;  // it also reads the current round
+	if (L > 0)
+		return lit + 8 * ((L - 1) >> 3) + 8 <= n;
+	if (pml <= 0)
+		return false;  // the previous match is not known here
+	const int32_t f = n1 + pmd, raw = f - pof, pad = (8 - (pml & 7)) & 7;
+	bool ok = raw >= 0 ? pml <= pof && pof - pml >= pad
+	                   : pof - f >= pml && oph - pof >= 8 && raw + pml + pad <= 0;
+	const int32_t q = pmd - pof + pml;  // the previous match's source end
+	ok = ok && q + pad <= max(glo, 0);  // the history region, or flushed to HBM before this batch
+	if (ok)
+		lit = ((q + D1_QBIAS) << 3) | pad;
+	return ok;
+}
+
 // One block.  hist: output bytes right before this block's slot that its
 // matches may read -- 0 for independent blocks; in a linked frame, the
 // earlier blocks' output, contiguous when every one of them is full.
@@ -1443,7 +1558,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
                                                 uint32_t b, const uint8_t* __restrict__ tab_all,
                                                 uint8_t* __restrict__ out,
                                                 lz4ada_block_status* __restrict__ status,
-                                                int64_t hist, int32_t& out_len, const bool ZL = false)
+                                                int64_t hist, int32_t& out_len, const bool ZL = false,
+                                                const bool D1E = false)
 {
 	const int32_t lane = int32_t(lane_id());
 	const lz4ada_block_desc d = desc[b];
@@ -1528,6 +1644,16 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 	int32_t o_batch = 0;  // output position of the current batch
 	bool bad = false;
 	bool d1 = false;  // a match with offset >= D1_OFF reads before the block start
+	// the host's prediction of the round state (linked bulk path): quirk D1
+	// emulated under it (d1x: a D1 match it cannot emulate declines the
+	// block; the status says AUX_D1_EMU: decoded under the prediction)
+	const bool d1p = D1E && (d.flags & BLOCK_D1_ROUND) != 0;  // (D1E: the linked planes' kernels)
+	const int32_t oph = int32_t(HISTORY_SIZE) + int32_t((d.flags >> BLOCK_D1_OPH_SHIFT) & 7u);
+	const int32_t n1 = int32_t(d.flags >> BLOCK_N1_SHIFT);
+	bool d1x = false;
+	// the previous batch's last match (block-relative output start, offset,
+	// length; pml = 0: none known) for a D1 match without literals in lane 0
+	int32_t pmd_b = 0, pof_b = 0, pml_b = 0;
 	bool deep = false;  // ZL: a match reads history positions below 256
 	int32_t hcnt = 0;   // ZL: match bytes read straight from the history region
 	for (int32_t k0 = 0; k0 < nsub && !bad;) {
@@ -1596,6 +1722,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				break;
 			}
 			o_batch += total;
+			pml_b = 0;  // (its sequences are not tracked for quirk D1)
 			vm_wait();
 			ICOUNT(D_GBATCHES, 1);
 			// reload the ring's history from HBM
@@ -1653,6 +1780,28 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					rdst[r] = o_round + inc - len;  // literal destination
 					o_round += __shfl(inc, 63);
 					const int32_t mdst = rdst[r] + rL[r];
+					if (d1p) {
+						// the previous sequence's match: lane - 1, lane 0 the
+						// previous round's lane 63 or the previous batch's last
+						int32_t pmd = __shfl(mdst, (lane + 63) & 63), pof = __shfl(roff[r], (lane + 63) & 63),
+						        pml = __shfl(rml[r], (lane + 63) & 63);
+						if (r > 0) {
+							const int32_t a = __shfl(rdst[0] + rL[0], 63), b = __shfl(roff[0], 63),
+							              c = __shfl(rml[0], 63);
+							if (lane == 0) {
+								pmd = a;
+								pof = b;
+								pml = c;
+							}
+						} else if (lane == 0) {
+							pmd = pmd_b;
+							pof = pof_b;
+							pml = pml_b;
+						}
+						if (rml[r] > 0 && !d1_emulable(mdst, rL[r], rlit[r], roff[r], rml[r], pmd, pof, pml, n1,
+						                               oph, n, glo))
+							d1x = true;
+					}
 					if (rml[r] > 0) {
 						if (roff[r] > mdst + hb)
 							pre = true;  // reference before the block start (D2) / history
@@ -1668,9 +1817,16 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				}
 			}
 		}
-		if (__any(pre)) {
+		if (__any(pre || d1x)) {
 			bad = true;
 			break;
+		}
+		if (d1p) {  // the batch's last sequence, for the next batch's lane 0
+			const int32_t l = (N - 1) & 63;
+			const bool r1 = N > 64;
+			pmd_b = __shfl(r1 ? rdst[1] + rL[1] : rdst[0] + rL[0], l);
+			pof_b = __shfl(r1 ? roff[1] : roff[0], l);
+			pml_b = __shfl(r1 ? rml[1] : rml[0], l);
 		}
 		ISTAMP(D_WALK2);
 
@@ -1704,11 +1860,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #pragma unroll
 					for (int c = 0; c < GC; ++c)
 						if (g && 16 * c < rml[r])
-#ifdef LZ4ADA_IDX_EXP_NOVG  // timing experiment: no HBM match loads (wrong output)
-							vg[r][c] = u32x4{uint32_t(src), 0u, 0u, 0u};
-#else
 							__builtin_memcpy(&vg[r][c], ob + src + 16 * c, 16);
-#endif
 					nc[r] = g ? max(((rml[r] + 15) >> 4) - GC, 0) : 0;
 					GCOUNT(0, __popcll(__ballot(g)));
 					GCOUNT(1, __popcll(__ballot(g)) + __popcll(__ballot(g && ((src & 127) > 112))));
@@ -1742,11 +1894,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				if (lane < tot) {
 					rpd = od + 16 * k;
 					rpn = min(16, oml - 16 * k);
-#ifdef LZ4ADA_IDX_EXP_NOVG
-					vr = u32x4{uint32_t(od - ooff), 0u, 0u, 0u};
-#else
 					__builtin_memcpy(&vr, ob + (od - ooff) + 16 * k, 16);
-#endif
 				}
 				wave_lds_fence();  // ldesc / own[] are written again later
 			}
@@ -1759,7 +1907,6 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		// its run from an LDS descriptor.  (Storing a short last piece as 16
 		// bytes that spill into its own match, rewritten in M, measured no
 		// faster.)
-#ifndef LZ4ADA_IDX_EXP_NOLIT
 		static_assert(RMAX == 2, "literal dealing pairs two rounds");
 		{
 #pragma unroll
@@ -1793,7 +1940,6 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				}
 			}
 		}
-#endif
 		wave_lds_fence();
 		ISTAMP(D_LIT);
 
@@ -1814,21 +1960,44 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		// them makes each later reuse of its registers wait vmcnt(0) (one
 		// showed up inside the near-match loop)
 		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#ifndef LZ4ADA_IDX_EXP_NOHBMST
 		// pieces of HBM-sourced matches beyond the first GC, dealt and
 		// loaded in P (the first 64 of the batch)
 		ostore(D, rpd, vr, rpn);  // (rpn = 0: none)
-#endif
 #pragma unroll
 		for (int r = 0; r < RMAX; ++r) {
 			mring[r] = oring[r] = lring[r] = 0;
 			if (64 * r < N) {
 				const int32_t mdst = rdst[r] + rL[r], off = roff[r], ml = rml[r];
 				const bool hbm = ml > 0 && mdst - off < glo;
-#ifndef LZ4ADA_IDX_EXP_NOHBMST  // timing experiment (wrong output): no HBM-sourced stores
 				static_assert(GC == 1, "one own HBM piece per match");
 				ostore(D, mdst, vg[r][0], hbm ? min(16, ml) : 0);
-#endif
+				if (d1p) {
+					// quirk D1 (d1_emulable): the match's first k1 bytes are
+					// what the last wild copy left past the frontier, from d =
+					// OPH - off on -- the payload bytes after its literals, or
+					// (no literals) the output bytes after the previous
+					// match's source, which P put in rlit (a D1 match reads
+					// >= 65,529 back: always HBM-sourced, stored above)
+					int32_t k1 = 0, sp = S.lo, gq = 0;
+					bool fo = false;
+					if (ml > 0 && n1 + mdst < off && oph - off < 8) {
+						const int32_t dd = oph - off;
+						const int32_t ovs = rL[r] > 0 ? 8 * ((rL[r] + 7) >> 3) - rL[r] : rlit[r] & 7;
+						if (dd < ovs) {
+							k1 = min(ovs - dd, ml);
+							if (rL[r] > 0) {
+								sp = rlit[r] + rL[r] + dd;
+							} else {
+								gq = (rlit[r] >> 3) - D1_QBIAS + dd;
+								fo = true;
+							}
+						}
+					}
+					u32x4 v = ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, sp);
+					if (fo)
+						__builtin_memcpy(&v, ob + gq, 16);
+					ostore(D, mdst, v, k1);
+				}
 				if (rtot[r] > rfirst[r]) {  // rare: more than 64 dealt pieces; the rest now
 					const int32_t nc = hbm ? max(((ml + 15) >> 4) - GC, 0) : 0;
 					const int32_t inc = wave_incl_scan(nc);
@@ -1861,10 +2030,9 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		// together; rounds of short ones only (e.g. dense data) keep one lane
 		// per match -- the dealing's fixed cost (owner search, dependency
 		// masks) would dominate there
-#ifndef LZ4ADA_IDX_EXP_NORING  // timing experiment (wrong output): no ring-sourced matches
 		static_assert(RMAX == 2, "ring dealing pairs two rounds");
 		if (__any(lring[0] > RING_LANE_MAX || lring[1] > RING_LANE_MAX)) {
-			const int32_t st = ring_pieces(D, mring, oring, lring, o_batch);
+			const int32_t st = ring_pieces(D, mring, oring, lring, o_batch, glo);
 			ICOUNT(D_TASKS, 1);
 			ICOUNT(D_ROUNDS, st);
 			(void)st;
@@ -1872,14 +2040,13 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
 				if (64 * r < N) {
-					const int32_t st = ring_lanes(D, mring[r], oring[r], lring[r], rbeg[r], rL[r]);
+					const int32_t st = ring_lanes(D, mring[r], oring[r], lring[r], rbeg[r], rL[r], glo);
 					ICOUNT(D_GBATCHES, 1);
 					ICOUNT(D_LANES, st);
 					(void)st;
 				}
 			}
 		}
-#endif
 		ISTAMP(D_NEAR);
 
 		// flush whole 16-byte units of [o_batch, o_end) (the first may start
@@ -1911,7 +2078,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 			status[b].code = DS_RETRY;
 		} else {
 			status[b].code = DS_OK;
-			status[b].aux = (d1 ? AUX_D1_RISK : 0) | (deep ? AUX_DEEP_HIST : 0);
+			status[b].aux = (d1 ? AUX_D1_RISK : 0) | (d1p ? AUX_D1_EMU : 0) | (deep ? AUX_DEEP_HIST : 0);
 			status[b].detail = ZL ? hcnt : 0;  // ZL: the linked path's density estimate
 			status[b].err_out_pos = 0;
 			status[b].out_len = uint32_t(o_batch);
@@ -1997,7 +2164,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	if (blockIdx.x >= nblocks)
 		return;
 	int32_t len;
-	decode_block(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, LINK_HIST, len, true);
+	decode_block(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, LINK_HIST, len, true, true);
+}
+
+// The linked path's byte planes (x, and y / h when a block needs them):
+// pass 2 of every block in the history layout with quirk D1 emulated under
+// the host's predicted round state (decode_block's D1E; k_decode_idx's
+// linked 2 mode without it).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_decode_idx_lk(
+        const uint8_t* __restrict__ frame, uint64_t frame_len, const lz4ada_block_desc* __restrict__ desc,
+        uint32_t nblocks, uint8_t* __restrict__ tab_all, uint8_t* __restrict__ out,
+        lz4ada_block_status* __restrict__ status)
+{
+	__shared__ DecLds D;
+	if (blockIdx.x >= nblocks)
+		return;
+	int32_t len;
+	decode_block(D, frame, frame_len, desc, blockIdx.x, tab_all, out, status, LINK_HIST, len, false, true);
 }
 
 // ============================================================ two waves
@@ -3180,12 +3363,12 @@ __device__ __forceinline__ int32_t decode_block_pp2(PpLds2& L, const uint8_t* __
 		}
 		static_assert(RMAX == 2, "ring dealing pairs two rounds");
 		if (__any(lring[0] > RING_LANE_MAX || lring[1] > RING_LANE_MAX)) {
-			ring_pieces(V, mring, oring, lring, ob0);
+			ring_pieces(V, mring, oring, lring, ob0, ob0 - RFLOOR2);
 		} else {
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r)
 				if (64 * r < N)
-					ring_lanes(V, mring[r], oring[r], lring[r], rbeg[r], rL[r]);
+					ring_lanes(V, mring[r], oring[r], lring[r], rbeg[r], rL[r], ob0 - RFLOOR2);
 		}
 		lds_publish(&L.tok, jb);
 
@@ -3345,6 +3528,11 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 		return hipSuccess;
 	if (mode == 6) {  // pass 2, linked layout, literals as zeros (k_decode_idx_zl)
 		hipLaunchKernelGGL(idx::k_decode_idx_zl, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
+		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
+		return hipGetLastError();
+	}
+	if (mode == 2) {  // pass 2, linked layout (k_decode_idx_lk: quirk D1 emulated)
+		hipLaunchKernelGGL(idx::k_decode_idx_lk, dim3(nblocks), dim3(64), 0, stream, d_frame, frame_len,
 		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
 		return hipGetLastError();
 	}

@@ -32,6 +32,21 @@ constexpr int32_t LINK_HIST = 65535;
 // DS_OK block) and the host sends those frames to the exact path.
 constexpr int32_t D1_OFF = int32_t(HISTORY_SIZE) - 7;
 constexpr int32_t AUX_D1_RISK = 1;
+// Quirk D1 in the linked bulk path, emulated (round 6): the host predicts
+// each block's round state from the slot sizes (every block full) and
+// passes it in the descriptor's flags -- BLOCK_D1_ROUND: the block's round
+// follows one that ended at Output_Pos_History = 65536 + the 3 bits at
+// BLOCK_D1_OPH_SHIFT; bits from BLOCK_N1_SHIFT: Output_Pos at the block's
+// start (its place in the round).  The index decoder then writes a D1
+// match's first bytes as the reference's wild literal copy leaves them
+// (lz4ada.adb:811-817, 862-879; the lone decoder's k_lone_words does the
+// same); its status carries AUX_D1_EMU (decoded under a prediction), and
+// the host accepts such a block only if the real round state equals the
+// prediction.  (Bits 0-1 are the public flags.)
+constexpr uint32_t BLOCK_D1_ROUND = 8u;
+constexpr int BLOCK_D1_OPH_SHIFT = 4;
+constexpr int BLOCK_N1_SHIFT = 16;
+constexpr int32_t AUX_D1_EMU = 4;
 // the linked path's literal-zero decode (k_decode_idx_zl): a match reads
 // history positions below 256, whose high byte is 0 like a literal's
 constexpr int32_t AUX_DEEP_HIST = 2;

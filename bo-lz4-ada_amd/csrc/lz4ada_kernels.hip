@@ -614,19 +614,8 @@ __device__ __forceinline__ uint32_t win_next(uint32_t t, uint32_t p)
 }
 
 // Consumer: copy batch `c` (records, output at o) into outb and flush it.
-// Timing experiments only (wrong output): LZ4ADA_EXP_ALIGNST stores every
-// copy chunk as one aligned 16-byte write, LZ4ADA_EXP_ALIGNLD reads literal
-// chunks from aligned addresses -- the cost of unaligned LDS access.
-#ifdef LZ4ADA_EXP_ALIGNST
-#define PC_STORE_N(p, v, n) (*reinterpret_cast<u32x4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15)) = (v))
-#else
 #define PC_STORE_N(p, v, n) lds_store_n((p), (v), (n))
-#endif
-#ifdef LZ4ADA_EXP_ALIGNLD
-#define PC_LOAD16(dst, p) (*(dst) = *reinterpret_cast<const u32x4*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15)))
-#else
 #define PC_LOAD16(dst, p) __builtin_memcpy((dst), (p), 16)
-#endif
 
 __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* __restrict__ ob,
                                               int32_t hist STAMP_PARAM)
@@ -652,21 +641,15 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 	u32x4 pv0 = {0, 0, 0, 0}, pv1 = {0, 0, 0, 0};
 	const bool pre0 = tl && tml > 0 && toff >= 16 && q0 + 16 <= o;
 	const bool pre1 = pre0 && tml > 16 && q0 + 32 <= o;
-#ifndef LZ4ADA_EXP_NOGLOBAL
 	if (pre0)
 		__builtin_memcpy(&pv0, (const uint8_t*)(ob + q0), 16);
 	if (pre1)
 		__builtin_memcpy(&pv1, (const uint8_t*)(ob + q0 + 16), 16);
-#endif
 	constexpr int32_t LONG = 48;
 	if (tL <= LONG) {
 		for (int32_t i = 0; i < tL; i += 16) {
 			u32x4 v;
-#ifdef LZ4ADA_EXP_LITU
-			v = ld16u(L.inb, uint32_t(tlit + i + mis) & INB_MASK, INB);
-#else
 			PC_LOAD16(&v, &L.inb[(tlit + i + mis) & INB_MASK]);
-#endif
 			PC_STORE_N(&outb[ts + i], v, tL - i);
 		}
 	}
@@ -675,11 +658,7 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 		const int32_t Lk = __shfl(tL, k), litk = __shfl(tlit, k), tsk = __shfl(ts, k);
 		for (int32_t i = 16 * lane; i < Lk; i += 1024) {
 			u32x4 v;
-#ifdef LZ4ADA_EXP_LITU
-			v = ld16u(L.inb, uint32_t(litk + i + mis) & INB_MASK, INB);
-#else
 			PC_LOAD16(&v, &L.inb[(litk + i + mis) & INB_MASK]);
-#endif
 			PC_STORE_N(&outb[tsk + i], v, Lk - i);
 		}
 	}
@@ -724,11 +703,7 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 					} else if (sp >= o - 16) {  // this batch or the tail before it
 						v = ld16u(L.outx, uint32_t(sp - o + 16), PC_OUTX);
 					} else {
-#ifdef LZ4ADA_EXP_NOGLOBAL
-						v = pv0;
-#else
 						__builtin_memcpy(&v, (const uint8_t*)(ob + sp), 16);
-#endif
 					}
 					PC_STORE_N(&outb[d0 + i], v, nn);
 				}
@@ -758,11 +733,7 @@ __device__ __forceinline__ void pc_copy_batch(PcLds& L, int c, int32_t mis, g8* 
 		const int32_t nv = (blen - h) / 16;
 		for (int32_t i = lane; i < nv; i += 64) {
 			u32x4 v;
-#ifdef LZ4ADA_EXP_LITU
-			v = ld16u(L.outx, uint32_t(16 + h + 16 * i), PC_OUTX);
-#else
 			__builtin_memcpy(&v, &outb[h + 16 * i], 16);
-#endif
 			*reinterpret_cast<GLOBAL u32x4*>(dst + h + 16 * i) = v;
 		}
 		for (int32_t i = h + nv * 16 + lane; i < blen; i += 64)

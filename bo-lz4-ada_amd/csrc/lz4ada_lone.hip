@@ -569,10 +569,15 @@ struct SeqRec {
 // (every older write ended before p - L, its overshoot before p).  So the
 // match's first k1 = ovs - d bytes (d < ovs) are those payload bytes -- lit
 // + L + d + j -- and the rest are history; its own chunks read ahead of
-// what they write.  Declined (exact path) instead: no literals (the last
-// write was a match, whose overshoot is a Buffer source), a literal run
-// whose last chunk was not wild (the payload's last 8 bytes), a match that
-// also reads the current round (p + ml > off).
+// what they write.  With no literals the last write was the previous
+// match's last Write_Output call, whose overshoot is the Buffer bytes right
+// after its source: emulated (as pointer words to those output positions,
+// kept in the record's lit) when that match was one call whose tail read
+// only final bytes -- the rule of lz4ada_idx.hip d1_emulable.  Declined
+// (exact path) instead: a literal run whose last chunk was not wild (the
+// payload's last 8 bytes), a match that also reads the current round (p +
+// ml > off), a no-literal read after any other previous match (or the
+// window's first sequence).
 
 template <int32_t LW>
 __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ blk, int32_t n,
@@ -699,9 +704,12 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 		tw += wred[1][j];
 	}
 	const uint32_t wo = obase[w];
+	for (int32_t j = si; j < min(sj, MAXSEQ); ++j)
+		R[j].o += ob;
+	if (d1 > 1)
+		__syncthreads();  // R[j - 1] of another thread, for quirk D1 below
 	for (int32_t j = si; j < min(sj, MAXSEQ); ++j) {
-		const uint32_t o = R[j].o + ob;
-		R[j].o = o;
+		const uint32_t o = R[j].o;
 		const int32_t L = R[j].L;
 		const int64_t off = int64_t(R[j].off), oa = int64_t(wo) + o;
 		if (off && oa + L + H < off) {
@@ -714,8 +722,22 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 			const int32_t d = d1 - int32_t(off);
 			const int32_t c_last = R[j].lit + 8 * ((L - 1) / 8);  // the literal copy's last chunk
 			const int32_t ovs = 8 * ((L + 7) / 8) - L;
-			if (L == 0 || c_last + 8 > n || n1 + oa + L + R[j].ml > off) {
+			if (n1 + oa + L + R[j].ml > off || (L > 0 && c_last + 8 > n)) {
 				bad = true;  // the cases not emulated: the exact path
+			} else if (L == 0) {
+				// the previous match's overshoot: output bytes q + d + i
+				const int32_t pml = j > 0 ? R[j - 1].ml : 0, pof = j > 0 ? int32_t(R[j - 1].off & 0xFFFFu) : 0;
+				const int32_t pmd = j > 0 ? int32_t(wo + R[j - 1].o) + R[j - 1].L : 0;
+				const int32_t f = n1 + pmd, raw = f - pof, pad = (8 - (pml & 7)) & 7;
+				const bool ok = pml > 0 && (raw >= 0 ? pml <= pof && pof - pml >= pad
+				                                     : pof - f >= pml && d1 - pof >= 8 && raw + pml + pad <= 0);
+				if (!ok) {
+					bad = true;
+				} else if (d < pad) {
+					const int32_t k1 = min(pad - d, R[j].ml);
+					R[j].lit = H + pmd - pof + pml + d;  // the word of output byte q + d
+					R[j].off = uint32_t(off) | (uint32_t(k1) << 16);
+				}
 			} else if (d < ovs) {
 				const int32_t k1 = min(ovs - d, R[j].ml);
 				R[j].off = uint32_t(off) | (uint32_t(k1) << 16);
@@ -779,8 +801,8 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 				uint32_t v;
 				if (j < 0)
 					v = LIT | S.at(r.lit + int32_t(x));
-				else if (uint32_t(j) < k1)  // quirk D1: the literals' overshoot
-					v = LIT | S.at(r.lit + r.L + (d1 - int32_t(off)) + j);
+				else if (uint32_t(j) < k1)  // quirk D1: the last wild copy's overshoot
+					v = r.L > 0 ? LIT | S.at(r.lit + r.L + (d1 - int32_t(off)) + j) : uint32_t(r.lit + j);
 				else
 					v = uint32_t(H) + oa - off;
 				W[oa] = v;

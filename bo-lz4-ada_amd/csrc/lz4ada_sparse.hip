@@ -558,23 +558,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 	// HBM -> HBM (runs longer than the staged window).  The stores are left
 	// in flight.
 	auto copy_lit = [&](int32_t lit, int32_t L, int32_t dst) {
-#ifdef LZ4ADA_SP_EXP_NOCOPY  // timing experiment (wrong output)
-		return;
-#endif
 		if (L <= 0)
 			return;
 		if (lit + mis >= vlo * STG && lit + L + mis <= shi && lit + L <= rbad) {
 			for (int32_t c = 0; c < L; c += 1024) {
 				const int32_t k = c + 16 * lane;
-#ifdef LZ4ADA_SP_EXP_NOSTORE  // timing experiment (wrong output): the reads only
-				if (k < L) {
-					const u32x4 v = ring16(S.ring, uint32_t(lit + mis + k));
-					asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-				}
-#else
 				if (k < L)
 					lit_store(ob, dst + k, ring16(S.ring, uint32_t(lit + mis + k)), L - k, cap);
-#endif
 				nvm += 1;
 			}
 			return;
@@ -690,7 +680,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 					// run repeat the last one, so no lane is masked off; the bytes a
 					// piece spills past the run are rewritten later)
 					const int32_t last = max((L - 1) >> 4, 0);
-#ifndef LZ4ADA_SP_EXP_NOCOPY  // timing experiment (wrong output)
 					{
 						const int32_t j = min(lane, last);
 						const u32x4 v = ring16(S.ring, uint32_t(lit + mis + 16 * j));
@@ -706,7 +695,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 						nvm += 3;
 					}
 					nvm += 1;
-#endif
 					const bool mine = lane == vns;
 					m_dst = mine ? vo + L : m_dst;
 					m_off = mine ? off : m_off;

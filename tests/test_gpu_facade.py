@@ -335,10 +335,47 @@ def test_facade_linked_d1_block_after_small_block(mid_len, lit_len, off):
         assert exact <= 1, exact
 
 
+def d1_frame_l0(lit_len, pof, pml, off, tail=b"vwxyz"):
+    """A 64 KiB block, then lit_len literals, a match of pml bytes pof back,
+    and a match `off` back with NO literals (quirk D1 after a match: the
+    last write's overshoot is the Buffer bytes after that match's source)."""
+    import struct
+    comp0, raw0 = lz4ada.gen_block(1, 1234, 65536)
+    lits = bytes(range(65, 65 + lit_len))
+    tok = (min(lit_len, 15) << 4) | (pml - 4)
+    ext = bytes([lit_len - 15]) if lit_len >= 15 else b""
+    comp1 = (bytes([tok]) + ext + lits + struct.pack("<H", pof) + bytes([0x06]) + struct.pack("<H", off) +
+             bytes([len(tail) << 4]) + tail)
+    frame, _ = lz4frame.build_frame([(comp0, raw0, False), (comp1, b"", False)], 64 * KiB, indep=False)
+    return frame
+
+
+# (literals, previous match offset, its length, D1 offset): the previous
+# match inside the round (its source ends >= its overshoot before its
+# output) or all from history (its tail stays in the previous round)
+D1_L0_SHAPES = [(16, 16, 4, 65533), (16, 16, 5, 65534), (16, 16, 9, 65530), (16, 16, 9, 65535),
+                (16, 16, 12, 65535), (16, 16, 7, 65535), (16, 16, 8, 65533),
+                (3, 1000, 10, 65534), (3, 40000, 4, 65535), (3, 20, 9, 65530), (3, 65528, 5, 65535)]
+
+
+@pytest.mark.parametrize("lit_len,pof,pml,off", D1_L0_SHAPES)
+def test_facade_linked_d1_without_literals_on_gpu(lit_len, pof, pml, off):
+    """Quirk D1 right after a match (no literals before the D1 read): the
+    lone decoder points the read's first bytes at the output bytes after the
+    previous match's source (what its last wild copy left past the
+    frontier, lz4ada.adb:811-817, 845-904), so the block stays on the GPU
+    and gives the reference's bytes, call by call."""
+    frame = d1_frame_l0(lit_len, pof, pml, off)
+    for feed in (0, 4096):
+        ours, exact = trace_ours_ctx(frame, feed)
+        assert ours == trace_oracle(frame, feed)
+        assert exact == 0, exact
+
+
 def test_facade_linked_d1_without_literals_goes_exact():
-    """Quirk D1 after a match rather than literals (the last write's
-    overshoot comes from the Buffer): not emulated -- the exact path, the
-    reference's bytes."""
+    """Quirk D1 after a match whose source overlaps its output (offset 3,
+    5 bytes: a repeating part, whose overshoot reads bytes that same call
+    wrote): not emulated -- the exact path, the reference's bytes."""
     import struct
     comp0, raw0 = lz4ada.gen_block(1, 1234, 65536)
     # 8 literals + a short match, then a sequence with no literals whose

@@ -109,28 +109,152 @@ def matches(payload):
         o += ml + 4
 
 
-def d1_risk(blocks):
-    """Whether the host's D1 rule (lz4ada_bulk_linked.cpp bulk_linked) must send the
-    frame to the exact path: a block starting right after Output_Pos_History
-    was set to 65536..65542 (lz4ada.adb:678-690, 785-787) with a match of
-    offset >= 65529 reaching before the block start."""
-    opos = oph = 0
-    for comp, raw in blocks:
+def d1_matches(payload, n1, oph):
+    """(L, lit, match output position, offset, ml, previous match) of the
+    block's matches in quirk D1's domain for round state (n1, oph): a read
+    before the round start within 7 bytes of where the last round ended.
+    The previous match is (output position, offset, ml), None for the
+    block's first sequence."""
+    i, o, n = 0, 0, len(payload)
+    prev = None
+    while i < n:
+        t = payload[i]
+        i += 1
+        L = t >> 4
+        if L == 15:
+            while True:
+                b = payload[i]
+                i += 1
+                L += b
+                if b != 255:
+                    break
+        lit = i
+        i += L
+        if i >= n:
+            return
+        off = payload[i] | (payload[i + 1] << 8)
+        i += 2
+        ml = t & 15
+        if ml == 15:
+            while True:
+                b = payload[i]
+                i += 1
+                ml += b
+                if b != 255:
+                    break
+        ml += 4
+        m = o + L
+        if n1 + m < off and oph - off < 8:
+            yield L, lit, m, off, ml, prev
+        prev = (m, off, ml)
+        o = m + ml
+
+
+def d1_emulable(payload, n1, oph):
+    """Whether the index decoder emulates every D1 read of the block under
+    round state (n1, oph) (lz4ada_idx.hip d1_emulable): "yes", "no", or
+    "maybe" where it depends on where the decoder's batch starts (a read
+    without literals copies the bytes after the previous match's source,
+    which must be in the history region or flushed to HBM: below the batch
+    start - 4,096)."""
+    res = "yes"
+    for L, lit, m, off, ml, prev in d1_matches(payload, n1, oph):
+        if n1 + m + ml > off:
+            return "no"
+        if L > 0:
+            if lit + 8 * ((L - 1) // 8) + 8 > len(payload):
+                return "no"
+            continue
+        if prev is None:
+            return "no"
+        pm, po, pml = prev
+        f, pad = n1 + pm, (8 - pml % 8) % 8
+        raw = f - po
+        ok = (pml <= po and po - pml >= pad) if raw >= 0 else \
+            (po - f >= pml and oph - po >= 8 and raw + pml + pad <= 0)
+        q = pm - po + pml
+        if not ok or q + pad > max(m - 4096, 0):
+            return "no"
+        if q + pad > max(m - 8176, 0):  # the batch start is in (m - 4080, m]
+            res = "maybe"
+    return res
+
+
+def batch_starts(blocks, bmax, budget):
+    """Block indices where lz4ada_bulk_linked.cpp's batches start (batches_of:
+    each block's slot, rounded to 256 bytes, plus its 64 KiB history region;
+    at least one block a batch)."""
+    starts, acc = [0], 0
+    for k, (comp, raw) in enumerate(blocks):
+        need = ((min(bmax, 255 * len(comp) + 64) + 255) & ~255) + 65536
+        if k > starts[-1] and acc + need > budget:
+            starts.append(k)
+            acc = 0
+        acc += need
+    return set(starts)
+
+
+def d1_stops(blocks, bmax, budget=None):
+    """The blocks the linked bulk path may hand to the exact path for quirk
+    D1 (lz4ada_bulk_linked.cpp bulk_linked): (the first certain one or None,
+    whether an earlier one depends on the decoder's batch cuts).  The host
+    predicts each block's round state (Output_Pos / Output_Pos_History,
+    lz4ada.adb:678-690, 785-787) with every block filling its slot; the
+    index decoder emulates D1 under the prediction where d1_emulable says so
+    (else it declines the block, and k_decode_pc decodes it without
+    emulation).  A block with a match >= 65529 back before its start goes
+    exact when it is in a D1 round and was not emulated under the real
+    state, or when it was emulated under a D1 prediction the real state
+    lacks.  Predictions restart from the real state at every batch
+    (LZ4ADA_LINKED_BATCH_BYTES)."""
+    budget = budget or int(os.environ.get("LZ4ADA_LINKED_BATCH_BYTES", 2 << 30))
+    starts = batch_starts(blocks, bmax, budget)
+    opos = oph = po = ph = 0
+    maybe = False
+    for k, (comp, raw) in enumerate(blocks):
+        if k in starts:  # each batch predicts from the real state at its start
+            po, ph = opos, oph
         if opos >= 65536:
             opos = 0
-        flag = any(off > q and off >= 65529 for q, off in matches(comp))
-        if flag and 65536 <= oph <= 65542:
-            return True
+        if po >= 65536:
+            po = 0
+        risk = any(off > q and off >= 65529 for q, off in matches(comp))
+        in_d1, pd1 = 65536 <= oph <= 65542, 65536 <= ph <= 65542
+        emu = d1_emulable(comp, po, ph) if pd1 else "no"
+        if risk:
+            exact = (po, ph) == (opos, oph)
+            if in_d1 and not (emu == "yes" and exact) and not (emu == "maybe" and exact):
+                return k, maybe
+            if in_d1 and emu == "maybe":
+                maybe = True
+            if not in_d1 and emu == "yes":
+                return k, maybe
+            if not in_d1 and emu == "maybe":
+                maybe = True
         opos += len(raw)
+        po += min(bmax, 255 * len(comp) + 64)
         if opos >= 65536:
             oph = opos
-    return False
+        if po >= 65536:
+            ph = po
+    return None, maybe
 
 
-def want_path(blocks):
-    """The linked bulk path takes the frame; at a D1 block the exact path
-    resumes and finishes it."""
-    return lz4ada.PATH_LINKED | (lz4ada.PATH_EXACT if d1_risk(blocks) else 0)
+def d1_stop(blocks, bmax, budget=None):
+    return d1_stops(blocks, bmax, budget)[0]
+
+
+def want_path(blocks, bmax, ok=True):
+    """The paths lz4ada_last_path() may report: the linked bulk path takes
+    the frame; at a block quirk D1 sends to the exact path, that path
+    resumes and finishes it.  ok=False (the reference raises at the end,
+    e.g. a content checksum its D1 bytes do not match): a bulk pass that
+    reaches the end hands the whole frame to the exact path for the
+    exception."""
+    stop, maybe = d1_stops(blocks, bmax)
+    L, E = lz4ada.PATH_LINKED, lz4ada.PATH_EXACT
+    done = L if ok else E
+    return {L | E} if stop is not None else ({done, L | E} if maybe else {done})
 
 
 # ------------------------------------------------------------ linked frames
@@ -152,7 +276,7 @@ def test_linked_frame_bulk(kind, bmax):
         with pytest.raises(lz4ada.LZ4AdaError) as ei:
             lz4ada.decode_frame(frame)
         assert str(ei.value) == O.exception_information(st, msg)
-    assert lz4ada.last_path() == want_path(blocks)
+    assert lz4ada.last_path() in want_path(blocks, bmax, st == O.OK)
 
 
 def test_linked_frame_mixed_block_sizes():
@@ -165,7 +289,7 @@ def test_linked_frame_mixed_block_sizes():
     assert st == O.OK and ref == raw, msg
     out, _ = lz4ada.decode_frame(frame)
     assert out == raw
-    assert lz4ada.last_path() == want_path(blocks)
+    assert lz4ada.last_path() in want_path(blocks, 256 * KiB)
 
 
 @pytest.mark.parametrize("batch", [None, 300 * KiB, 1])
@@ -199,15 +323,15 @@ def test_linked_word_modes(kind, words, batch, env):
         env("LZ4ADA_LINKED_BATCH_BYTES", str(batch))
     lens = [65536, 70001, 100, 65535, 131075, 3, 65536, 200001, 4097]
     frame, raw, blocks = linked_frame(lz4ada.GEN_KINDS[kind], lens, 256 * KiB, seed=17)
-    same_as_oracle(frame)
-    assert lz4ada.last_path() == want_path(blocks)
+    st, _ = same_as_oracle(frame)
+    assert lz4ada.last_path() in want_path(blocks, 256 * KiB, st == O.OK)
 
 
 def test_linked_small_batches_64k(env):
     env("LZ4ADA_LINKED_BATCH_BYTES", str(200 * KiB))
     frame, raw, blocks = linked_frame(lz4ada.GEN_MIXED, [65536] * 9 + [4000], 64 * KiB, seed=3)
-    same_as_oracle(frame)
-    assert lz4ada.last_path() == want_path(blocks)
+    st, _ = same_as_oracle(frame)
+    assert lz4ada.last_path() in want_path(blocks, 64 * KiB, st == O.OK)
 
 
 def d1_frame(content_cksum):
@@ -225,15 +349,51 @@ def d1_frame(content_cksum):
     return frame, spec
 
 
-def test_d1_goes_exact_and_matches_reference():
+def test_d1_emulated_in_bulk_matches_reference():
     frame, spec = d1_frame(content_cksum=False)
     st, ref, msg = oracle(frame)
     assert st == O.OK, msg
     assert ref != spec  # the reference really diverges here
     out, _ = lz4ada.decode_frame(frame)
     assert out == ref
-    # block 0 through the linked bulk path, the exact path from block 1 on
-    assert lz4ada.last_path() == lz4ada.PATH_LINKED | lz4ada.PATH_EXACT
+    # both blocks through the linked bulk path: block 1's D1 match emulated
+    # under the predicted round state (Output_Pos_History 65536, Output_Pos 0)
+    assert lz4ada.last_path() == lz4ada.PATH_LINKED
+
+
+def test_d1_uniform_offsets_64k_frame():
+    """LZ4F's default block mode (64 KiB linked) with uniform match offsets:
+    quirk D1 in ~1 block of 6 (tools/d1_frame_time.py's frame).  Emulated
+    in bulk, with the exact path only from the first block the decoder
+    cannot emulate; the bytes are the reference's."""
+    blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_MIXED, 0x4C5A3441, 64 * KiB, 64)
+    frame, _ = lz4frame.build_frame([(c, r, False) for c, r in blocks], 64 * KiB, indep=False)
+    st, ref, msg = oracle(frame)
+    assert st == O.OK, msg
+    out, _ = lz4ada.decode_frame(frame)
+    assert out == ref
+    assert lz4ada.last_path() in want_path(blocks, 64 * KiB)
+
+
+@pytest.mark.parametrize("lit_len,pof,pml,off", [(16, 16, 4, 65533), (16, 16, 9, 65535), (3, 1000, 10, 65534),
+                                                 (3, 40000, 4, 65535), (3, 20, 9, 65530)])
+def test_d1_without_literals_in_bulk(lit_len, pof, pml, off):
+    """Quirk D1 right after a match (test_gpu_facade.py's d1_frame_l0
+    shapes) through the linked bulk path: emulated where the previous
+    match's source tail is in the history region (k_decode_idx_lk reads it
+    from HBM), else the exact path takes the block; the reference's bytes
+    either way."""
+    from test_gpu_facade import d1_frame_l0
+    frame = d1_frame_l0(lit_len, pof, pml, off)
+    st, ref, msg = oracle(frame)
+    assert st == O.OK, msg
+    out, _ = lz4ada.decode_frame(frame)
+    assert out == ref
+    info, descs = lz4ada.frame_index(frame)
+    blocks = [(frame[d.in_off:d.in_off + d.in_len], b"\0" * (65536 if k == 0 else len(ref) - 65536))
+              for k, d in enumerate(descs[:info.nblocks])]
+    assert lz4ada.last_path() in want_path(blocks, 64 * KiB)
+    assert lz4ada.last_path() == (lz4ada.PATH_LINKED if lit_len == 3 else lz4ada.PATH_LINKED | lz4ada.PATH_EXACT)
 
 
 def test_d1_with_content_checksum_raises_like_reference():

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""CPU model of the bulk linked decoders' quirk-D1 emulation
+(lz4ada_idx.hip d1_emulable; lib/lz4ada.adb:811-817, 845-904), checked
+against the oracle (the reference's bytes): every block of a linked frame of
+64 KiB generator blocks is decoded on top of the oracle's output before it,
+with D1 reads emulated under the real round state -- after literals (payload
+bytes past them) and, optionally, without literals (the output bytes past the
+previous match's source).  Prints the emulated / declined counts and the
+blocks whose bytes differ from the oracle's (none expected).
+    python tools/d1_model.py [NBLOCKS] [KIND ...]"""
+import collections
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "bo-lz4-ada_amd"))
+import lz4ada, lz4frame
+import _oracle as O
+
+def seqs(comp):
+    i, n = 0, len(comp); out = []
+    while i < n:
+        t = comp[i]; i += 1; L = t >> 4
+        if L == 15:
+            while True:
+                b = comp[i]; i += 1; L += b
+                if b != 255: break
+        lit = i; i += L
+        if i >= n: out.append((L, lit, 0, 0)); break
+        off = comp[i] | (comp[i + 1] << 8); i += 2
+        ml = t & 15
+        if ml == 15:
+            while True:
+                b = comp[i]; i += 1; ml += b
+                if b != 255: break
+        out.append((L, lit, off, ml + 4))
+    return out
+
+def emulate(blocks, ref, l0=True):
+    """each block decoded on top of the reference's true output before it"""
+    opos = oph = 0; pos = 0; reasons = collections.Counter(); bad = []
+    for k, (comp, raw) in enumerate(blocks):
+        if opos >= 65536: opos = 0
+        in_d1 = 65536 <= oph <= 65542
+        n1 = opos; n = len(comp)
+        out = bytearray(ref[:pos]); start = pos; declined = None
+        prev = None  # (mdst_blk, off, ml) of the previous sequence's match
+        for (L, lit, off, ml) in seqs(comp):
+            out += comp[lit:lit + L]
+            if ml == 0: break
+            m = len(out) - start
+            k1 = 0; src = None
+            if in_d1 and n1 + m < off and oph - off < 8:
+                d = oph - off
+                if n1 + m + ml > off:
+                    declined = declined or "reads current round"
+                elif L > 0:
+                    if lit + 8 * ((L - 1) // 8) + 8 > n:
+                        declined = declined or "literal tail"
+                    ovs = 8 * ((L + 7) // 8) - L
+                    if d < ovs: k1 = min(ovs - d, ml); src = ("pay", lit + L + d); reasons["L>0 k1>0"] += 1
+                else:
+                    if prev is None:
+                        declined = declined or "L0 first in block"
+                    elif not l0:
+                        declined = declined or "L0"
+                    else:
+                        pm, po, pml = prev          # block coords
+                        f = n1 + pm                 # round coords
+                        raw_ = f - po
+                        pad = (8 - pml % 8) % 8
+                        if raw_ >= 0:
+                            if pml > po: declined = declined or "L0 prev R"
+                            elif po - pml < pad: declined = declined or "L0 prev overlap"
+                        else:
+                            if po - f < pml: declined = declined or "L0 prev H+I"
+                            elif oph - po < 8: declined = declined or "L0 prev D1"
+                            elif raw_ + pml + pad > 0: declined = declined or "L0 past prev round"
+                        q0 = pm - po + pml  # block coords
+                        if d < pad:
+                            k1 = min(pad - d, ml); src = ("out", q0 + d); reasons["L0 k1>0"] += 1
+                        else: reasons["L0 k1=0"] += 1
+            for j in range(ml):
+                if j < k1:
+                    if src[0] == "pay": out.append(comp[src[1] + j])
+                    else: out.append(out[start + src[1] + j])
+                else: out.append(out[len(out) - off])
+            prev = (m, off, ml)
+        blen = len(out) - start
+        if declined: reasons["declined " + declined] += 1
+        elif bytes(out[start:]) != ref[start:start + blen]: bad.append(k)
+        pos += len(raw); opos += len(raw)
+        if opos >= 65536: oph = opos
+    return reasons, bad
+
+nb = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+for kind in sys.argv[2:] or ["mixed"]:
+    blocks = lz4ada.gen_linked_blocks(lz4ada.GEN_KINDS[kind], 0x4C5A3441, 64 << 10, nb)
+    frame, _ = lz4frame.build_frame([(c, r, False) for c, r in blocks], 64 << 10, indep=False)
+    st, ref, msg = O.unlz4ada(frame, out_cap=nb * (64 << 10) + (1 << 20))
+    assert st == O.OK
+    for l0 in (False, True):
+        r, bad = emulate(blocks, ref, l0)
+        print(kind, "L0 emu" if l0 else "no L0", dict(r), "mismatching blocks:", bad[:10], len(bad))

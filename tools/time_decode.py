@@ -32,6 +32,7 @@ VARIANTS = {"pc": lz4ada.DECODE_PC,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kind", default="mixed")
+    ap.add_argument("--real", default="", help="t1111k / liblz4_text: encoder blocks (bench.real_sources)")
     ap.add_argument("--blocks", type=int, default=2048)
     ap.add_argument("--unique", type=int, default=16)
     ap.add_argument("--steps", type=int, default=5)
@@ -44,8 +45,12 @@ def main():
     dev = torch.device("cuda", 0)
     bmax = args.block_max
     M = (lz4ada, lz4frame, xxhash, torch)
-    recs = bench.make_unique_blocks(lz4ada, lz4frame, xxhash, args.kind, args.unique, bmax,
-                                    block_cksum=not args.no_bcksum)
+    if args.real:
+        recs = bench.real_sources(args.real)[0]
+        args.kind = args.real
+    else:
+        recs = bench.make_unique_blocks(lz4ada, lz4frame, xxhash, args.kind, args.unique, bmax,
+                                        block_cksum=not args.no_bcksum)
     d_frame, frame_len, d_desc, exp_hash, comp, raw, descs = bench.assemble_shard(
         lz4ada, torch, recs, 0, args.blocks, bmax, dev, slot_pad=args.slot_pad)
     d_out = torch.empty(args.blocks * (bmax + args.slot_pad), dtype=torch.uint8, device=dev)
