@@ -1518,7 +1518,7 @@ __device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_
 constexpr int32_t D1_QBIAS = 1 << 17;
 __device__ __forceinline__ bool d1_emulable(int32_t mdst, int32_t L, int32_t& lit, int32_t off, int32_t ml,
                                             int32_t pmd, int32_t pof, int32_t pml, int32_t n1, int32_t oph,
-                                            int32_t n, int32_t glo)
+                                            int32_t n)
 {
 	if (!(n1 + mdst < off && oph - off < 8))
 		return true;  // no D1 read
@@ -1532,7 +1532,6 @@ __device__ __forceinline__ bool d1_emulable(int32_t mdst, int32_t L, int32_t& li
 	bool ok = raw >= 0 ? pml <= pof && pof - pml >= pad
 	                   : pof - f >= pml && oph - pof >= 8 && raw + pml + pad <= 0;
 	const int32_t q = pmd - pof + pml;  // the previous match's source end
-	ok = ok && q + pad <= max(glo, 0);  // the history region, or flushed to HBM before this batch
 	if (ok)
 		lit = ((q + D1_QBIAS) << 3) | pad;
 	return ok;
@@ -1799,7 +1798,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 							pml = pml_b;
 						}
 						if (rml[r] > 0 && !d1_emulable(mdst, rL[r], rlit[r], roff[r], rml[r], pmd, pof, pml, n1,
-						                               oph, n, glo))
+						                               oph, n))
 							d1x = true;
 					}
 					if (rml[r] > 0) {
@@ -1971,13 +1970,18 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 				const bool hbm = ml > 0 && mdst - off < glo;
 				static_assert(GC == 1, "one own HBM piece per match");
 				ostore(D, mdst, vg[r][0], hbm ? min(16, ml) : 0);
+				int32_t xoff = off, xml = (ml > 0 && !hbm) ? ml : 0;  // its ring copy, if any
 				if (d1p) {
 					// quirk D1 (d1_emulable): the match's first k1 bytes are
 					// what the last wild copy left past the frontier, from d =
 					// OPH - off on -- the payload bytes after its literals, or
 					// (no literals) the output bytes after the previous
 					// match's source, which P put in rlit (a D1 match reads
-					// >= 65,529 back: always HBM-sourced, stored above)
+					// >= 65,529 back: always HBM-sourced, stored above).  Those
+					// output bytes: from HBM when flushed (below glo), else a
+					// ring copy of their own (offset mdst - q, k1 bytes) among
+					// the batch's ring matches, which orders it after the
+					// bytes' producers and before their readers
 					int32_t k1 = 0, sp = S.lo, gq = 0;
 					bool fo = false;
 					if (ml > 0 && n1 + mdst < off && oph - off < 8) {
@@ -1992,6 +1996,12 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 								fo = true;
 							}
 						}
+					}
+					if (fo && gq >= glo) {
+						xoff = mdst - gq;
+						xml = k1;
+						k1 = 0;
+						fo = false;
 					}
 					u32x4 v = ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, sp);
 					if (fo)
@@ -2017,8 +2027,8 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 				}
 				mring[r] = mdst;
-				oring[r] = off;
-				lring[r] = (ml > 0 && !hbm) ? ml : 0;
+				oring[r] = xoff;
+				lring[r] = xml;
 			}
 		}
 		// every HBM-sourced match of the batch is stored before the ring

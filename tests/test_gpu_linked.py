@@ -152,12 +152,9 @@ def d1_matches(payload, n1, oph):
 
 def d1_emulable(payload, n1, oph):
     """Whether the index decoder emulates every D1 read of the block under
-    round state (n1, oph) (lz4ada_idx.hip d1_emulable): "yes", "no", or
-    "maybe" where it depends on where the decoder's batch starts (a read
-    without literals copies the bytes after the previous match's source,
-    which must be in the history region or flushed to HBM: below the batch
-    start - 4,096)."""
-    res = "yes"
+    round state (n1, oph) (lz4ada_idx.hip d1_emulable): "yes" or "no".  A
+    read without literals copies the bytes after the previous match's source
+    (from HBM, or as a ring copy of its own when they are recent)."""
     for L, lit, m, off, ml, prev in d1_matches(payload, n1, oph):
         if n1 + m + ml > off:
             return "no"
@@ -172,12 +169,9 @@ def d1_emulable(payload, n1, oph):
         raw = f - po
         ok = (pml <= po and po - pml >= pad) if raw >= 0 else \
             (po - f >= pml and oph - po >= 8 and raw + pml + pad <= 0)
-        q = pm - po + pml
-        if not ok or q + pad > max(m - 4096, 0):
+        if not ok:
             return "no"
-        if q + pad > max(m - 8176, 0):  # the batch start is in (m - 4080, m]
-            res = "maybe"
-    return res
+    return "yes"
 
 
 def batch_starts(blocks, bmax, budget):
@@ -379,10 +373,9 @@ def test_d1_uniform_offsets_64k_frame():
                                                  (3, 40000, 4, 65535), (3, 20, 9, 65530)])
 def test_d1_without_literals_in_bulk(lit_len, pof, pml, off):
     """Quirk D1 right after a match (test_gpu_facade.py's d1_frame_l0
-    shapes) through the linked bulk path: emulated where the previous
-    match's source tail is in the history region (k_decode_idx_lk reads it
-    from HBM), else the exact path takes the block; the reference's bytes
-    either way."""
+    shapes) through the linked bulk path: the previous match's source tail
+    from the history region (HBM) or from this batch's output (a ring copy
+    of its own in k_decode_idx_lk); the reference's bytes, no exact path."""
     from test_gpu_facade import d1_frame_l0
     frame = d1_frame_l0(lit_len, pof, pml, off)
     st, ref, msg = oracle(frame)
@@ -393,7 +386,7 @@ def test_d1_without_literals_in_bulk(lit_len, pof, pml, off):
     blocks = [(frame[d.in_off:d.in_off + d.in_len], b"\0" * (65536 if k == 0 else len(ref) - 65536))
               for k, d in enumerate(descs[:info.nblocks])]
     assert lz4ada.last_path() in want_path(blocks, 64 * KiB)
-    assert lz4ada.last_path() == (lz4ada.PATH_LINKED if lit_len == 3 else lz4ada.PATH_LINKED | lz4ada.PATH_EXACT)
+    assert lz4ada.last_path() == lz4ada.PATH_LINKED
 
 
 def test_d1_with_content_checksum_raises_like_reference():

@@ -150,19 +150,29 @@ def test_linked_corrupted_data_without_block_checksum(seed):
     check_like_oracle(bytes(b))
 
 
-def test_d1_block_mid_frame_resumes_there():
-    """Quirk D1 in block 3 of 5: blocks 0-2 (ending at Output_Pos 65536) through the
-    linked bulk path, the exact path from block 3 with the real Buffer."""
+@pytest.mark.parametrize("shape", ["literals", "overlap"])
+def test_d1_block_mid_frame(shape):
+    """Quirk D1 in block 3 of 5, after blocks 0-2 that
+    end at Output_Pos 65536.  'literals': a 20-byte literal run, then the
+    read 65533 back -- emulated in the linked bulk path, the whole frame
+    there.  'overlap': the read follows a match whose source overlaps its
+    output (a repeating part, not emulated) -- blocks 0-2 through the bulk
+    path, the exact path from block 3 with the real Buffer."""
     import struct
     pre = lz4ada.gen_linked_blocks(lz4ada.GEN_MIXED, 5, 0, 0, lens=[30000, 20000, 15536])
-    lits = bytes(range(65, 85))
-    d1 = bytes([0xF6, 20 - 15]) + lits + struct.pack("<H", 65533) + bytes([0x50]) + b"vwxyz"
+    if shape == "literals":
+        lits = bytes(range(65, 85))
+        d1 = bytes([0xF6, 20 - 15]) + lits + struct.pack("<H", 65533) + bytes([0x50]) + b"vwxyz"
+    else:
+        d1 = (bytes([0x81]) + b"ABCDEFGH" + struct.pack("<H", 3) + bytes([0x06]) +
+              struct.pack("<H", 65533) + bytes([0x50]) + b"vwxyz")
     post = lz4ada.gen_block(1, 77, 40000)
     blocks = [(c, r, False) for c, r in pre] + [(d1, b"", False), (post[0], post[1], False)]
     frame, _ = lz4frame.build_frame(blocks, 64 << 10, indep=False, content_cksum=False)
     st, exc = check_like_oracle(frame)
     assert st == O.OK
-    assert lz4ada.last_path() == lz4ada.PATH_LINKED | lz4ada.PATH_EXACT
+    want = lz4ada.PATH_LINKED if shape == "literals" else lz4ada.PATH_LINKED | lz4ada.PATH_EXACT
+    assert lz4ada.last_path() == want
 
 
 def test_bulk_resume_checks_declared_content_size():
