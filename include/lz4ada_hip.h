@@ -161,10 +161,11 @@ int lz4ada_xxh32_hash(const uint8_t *data, int64_t len, uint32_t *out);
  * non-last block is full.  lz4ada_decode_frame() decodes independent
  * blocks this way; linked frames (and independent ones whose blocks read
  * earlier blocks, quirk D2) decode every block at once against a synthetic
- * history that the GPU then resolves.  A non-zero
- * block status, a failed checksum, quirk D1 or a reference before the frame
- * start sends the frame down the reference-exact serial path, which
- * reproduces the reference's output and exception.
+ * history that the GPU then resolves (quirk D1
+ * emulated there, section 6).  A non-zero block status, a failed checksum,
+ * a D1 read the GPU does not emulate or a reference before the frame start
+ * sends the frame (from that block on) down the reference-exact serial
+ * path, which reproduces the reference's output and exception.
  */
 
 typedef struct {
@@ -332,8 +333,9 @@ int lz4ada_decode_frame_partial(const uint8_t *frame, int64_t len, uint8_t **out
  * on the GPU, into contiguous device output d_out
  * (out_cap bytes); descs are the HOST descriptors from lz4ada_frame_index.
  * Synchronous on `stream`.  Returns LZ4ADA_EXACT_PATH when the reference
- * would raise or diverge (block error, checksum mismatch, quirk D1, a
- * reference before the frame start) -- lz4ada_decode_frame() then gives
+ * would raise or diverge in a way the GPU does not reproduce (block error,
+ * checksum mismatch, a quirk-D1 read it does not emulate, a reference
+ * before the frame start) -- lz4ada_decode_frame() then gives
  * the reference's result.  The content checksum is the caller's. */
 int lz4ada_decode_linked_device(const void *d_frame, uint64_t frame_len,
                                 const lz4ada_block_desc *descs, int64_t nblocks, int64_t block_max,
