@@ -24,7 +24,7 @@ TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
-REDUCED="--no-cpu-baseline --no-e2e --no-linked --no-64k --no-c3 --no-facade --classes="
+REDUCED="--no-cpu-baseline --no-e2e --no-linked --no-64k --no-c3 --no-facade --classes= --real="
 fail() { echo "step $1 failed"; tail -20 "$2" 2>/dev/null; exit 1; }
 for step in "$@"; do
   case $step in
