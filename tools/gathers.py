@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kinds", default="mixed")
     ap.add_argument("--blocks", type=int, default=2048)
+    ap.add_argument("--real", default="", help="t1111k,liblz4_text: encoder blocks (bench.real_sources)")
     args = ap.parse_args()
     import lz4frame
     import xxhash
@@ -33,8 +34,9 @@ def main():
     buf = (ctypes.c_ulonglong * 4)()
     dev = torch.device("cuda", 0)
     bmax = 4 << 20
-    for kind in args.kinds.split(","):
-        recs = bench.make_unique_blocks(lz4ada, lz4frame, xxhash, kind, 64, bmax)
+    for kind in (args.real.split(",") if args.real else args.kinds.split(",")):
+        recs = (bench.real_sources(kind)[0] if args.real else
+                bench.make_unique_blocks(lz4ada, lz4frame, xxhash, kind, 64, bmax))
         fr, fl, de, eh, cb, rb, _ = bench.assemble_shard(lz4ada, torch, recs, 0, args.blocks, bmax, dev)
         out = torch.empty(args.blocks * bmax, dtype=torch.uint8, device=dev)
         st = torch.zeros(args.blocks * 32, dtype=torch.uint8, device=dev)

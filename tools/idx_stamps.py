@@ -32,16 +32,18 @@ def main():
     ap.add_argument("--kinds", default="mixed")
     ap.add_argument("--blocks", type=int, default=2048)
     ap.add_argument("--block-max", type=int, default=4 << 20)
+    ap.add_argument("--real", default="", help="t1111k / liblz4_text: encoder blocks (bench.real_sources)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     bmax = args.block_max
     f = lz4ada._lib.lz4ada_idx_stamps
     f.argtypes = [ctypes.c_void_p, ctypes.c_int]
     buf = (ctypes.c_ulonglong * len(NAMES))()
-    for kind in args.kinds.split(","):
+    for kind in ([args.real] if args.real else args.kinds.split(",")):
         import lz4frame
         import xxhash
-        recs = bench.make_unique_blocks(lz4ada, lz4frame, xxhash, kind, 64, bmax)
+        recs = (bench.real_sources(kind)[0] if args.real else
+                bench.make_unique_blocks(lz4ada, lz4frame, xxhash, kind, 64, bmax))
         fr, fl, de, eh, cb, rb, _ = bench.assemble_shard(lz4ada, torch, recs, 0, args.blocks, bmax,
                                                          dev)
         out = torch.empty(args.blocks * bmax, dtype=torch.uint8, device=dev)
