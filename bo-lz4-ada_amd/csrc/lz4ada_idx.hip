@@ -275,6 +275,10 @@ __device__ __forceinline__ bool parse_seq(const Src& S, int32_t p, int32_t n, Se
 	return true;
 }
 
+#ifndef LZ4ADA_P_SPLIT
+#define LZ4ADA_P_SPLIT 0
+#endif
+
 // parse_seq for the common shape, without branches: both length
 // extensions at most one byte, every byte read in the LDS window, the
 // sequence well before the block end.  Anything else (and malformed data)
@@ -303,6 +307,31 @@ __device__ __forceinline__ bool parse_fast(const Src& S, int32_t p, int32_t n, S
 	if (__builtin_expect(ok, 1))
 		return true;
 	return parse_seq(S, p, n, q);
+}
+
+// parse_fast's branch-free form alone: false where it does not apply (the
+// caller then runs parse_seq for that sequence; q is a placeholder)
+__device__ __forceinline__ bool parse_fast_try(const Src& S, int32_t p, int32_t n, Seq& q)
+{
+	const uint32_t a = uint32_t(p + S.mis) & S.mask;
+	const uint32_t* wa = reinterpret_cast<const uint32_t*>(S.lds + (a & ~3u));
+	const uint32_t w = __builtin_amdgcn_alignbyte(wa[1], wa[0], a & 3u);
+	const uint32_t tk = w & 0xffu, e1 = (w >> 8) & 0xffu;
+	const bool x1 = tk >= 0xf0u, x2 = (tk & 15u) == 15u;
+	const int32_t L = int32_t(tk >> 4) + (x1 ? int32_t(e1) : 0);
+	const int32_t lit = p + 1 + (x1 ? 1 : 0);
+	const int32_t x = lit + L;
+	const uint32_t b = uint32_t(x + S.mis) & S.mask;
+	const uint32_t* wb = reinterpret_cast<const uint32_t*>(S.lds + (b & ~3u));
+	const uint32_t w2 = __builtin_amdgcn_alignbyte(wb[1], wb[0], b & 3u);
+	const uint32_t e2 = (w2 >> 16) & 0xffu;
+	q.lit = lit;
+	q.L = L;
+	q.off = int32_t(w2 & 0xffffu);
+	q.ml = int32_t(tk & 15u) + 4 + (x2 ? int32_t(e2) : 0);
+	q.next = x + 2 + (x2 ? 1 : 0);
+	return p >= S.lo && x + 8 <= S.hi && x + 8 <= n && !(x1 && e1 == 255u) && !(x2 && e2 == 255u) &&
+	       q.off != 0;
 }
 
 
@@ -1760,11 +1789,47 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		bool pre = false, anyg = false;
 		{
 			int32_t o_round = o_batch;
+#if LZ4ADA_P_SPLIT
+			// both rounds' sequences parsed first (their starts are known, so
+			// the four dependent LDS reads of the two rounds overlap), the
+			// rare shapes the branch-free form rejects after, then placement
+			bool fok[RMAX];
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
 				rL[r] = rlit[r] = roff[r] = rml[r] = 0;
+				fok[r] = true;
+				const int32_t idx = 64 * r + lane;
+				if (idx < N) {
+					Seq q;
+					fok[r] = parse_fast_try(S, base + int32_t(D.cst[idx]), n, q);
+					rL[r] = q.L;
+					rlit[r] = q.lit;
+					roff[r] = q.off;
+					rml[r] = q.ml;
+				}
+			}
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				if (__builtin_expect(__any(!fok[r]), 0)) {
+					if (!fok[r]) {
+						Seq q;
+						parse_seq(S, base + int32_t(D.cst[64 * r + lane]), n, q);
+						rL[r] = q.L;
+						rlit[r] = q.lit;
+						roff[r] = q.off;
+						rml[r] = q.ml;
+					}
+				}
+			}
+#endif
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+#if !LZ4ADA_P_SPLIT
+				rL[r] = rlit[r] = roff[r] = rml[r] = 0;
+#endif
 				rbeg[r] = o_round;
 				if (64 * r < N) {
+#if !LZ4ADA_P_SPLIT
 					const int32_t idx = 64 * r + lane;
 					if (idx < N) {
 						Seq q;
@@ -1774,6 +1839,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 						roff[r] = q.off;
 						rml[r] = q.ml;
 					}
+#endif
 					const int32_t len = rL[r] + rml[r];
 					const int32_t inc = wave_incl_scan(len);
 					rdst[r] = o_round + inc - len;  // literal destination
