@@ -678,9 +678,9 @@ def bench_linked(M, dev, sh, stream, kind="mixed", nblocks=4096, bmax=256 * 1024
             "frac": round((comp + raw) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "compressed_bytes": comp, "decoded_bytes": raw,
             "path": "lz4ada_decode_linked_device: block checksums (side stream), k_index, "
-                    "2 x k_decode_idx (every block at once: history plane X = k & 255, then "
-                    "plane Z with literals 0 and history k >> 8; a third plane only for blocks "
-                    "flagged deep), k_link_init (words and bytes) + k_link_jump rounds (history "
+                    "k_decode_idx_lk + k_decode_idx_zl concurrently (every block at once: history "
+                    "plane X = k & 255, plane Z with literals 0 and history k >> 8; quirk D1 emulated "
+                    "under the predicted round state; a third plane only for blocks flagged deep), k_link_init (words and bytes) + k_link_jump rounds (history "
                     "resolved on the GPU); wall clock of the whole call, device-resident frame "
                     "and output",
             "golden": "per-block XXH32 of the output vs the generator"}
