@@ -275,10 +275,6 @@ __device__ __forceinline__ bool parse_seq(const Src& S, int32_t p, int32_t n, Se
 	return true;
 }
 
-#ifndef LZ4ADA_P_SPLIT
-#define LZ4ADA_P_SPLIT 0
-#endif
-
 // parse_seq for the common shape, without branches: both length
 // extensions at most one byte, every byte read in the LDS window, the
 // sequence well before the block end.  Anything else (and malformed data)
@@ -1789,10 +1785,11 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		bool pre = false, anyg = false;
 		{
 			int32_t o_round = o_batch;
-#if LZ4ADA_P_SPLIT
 			// both rounds' sequences parsed first (their starts are known, so
 			// the four dependent LDS reads of the two rounds overlap), the
 			// rare shapes the branch-free form rejects after, then placement
+			// (mixed / dense / text -0.5..-0.9% against one round at a time,
+			// profiles/r06u_psplit_ab.txt; 189 VGPRs)
 			bool fok[RMAX];
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
@@ -1821,25 +1818,10 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 					}
 				}
 			}
-#endif
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
-#if !LZ4ADA_P_SPLIT
-				rL[r] = rlit[r] = roff[r] = rml[r] = 0;
-#endif
 				rbeg[r] = o_round;
 				if (64 * r < N) {
-#if !LZ4ADA_P_SPLIT
-					const int32_t idx = 64 * r + lane;
-					if (idx < N) {
-						Seq q;
-						parse_fast(S, base + int32_t(D.cst[idx]), n, q);
-						rL[r] = q.L;
-						rlit[r] = q.lit;
-						roff[r] = q.off;
-						rml[r] = q.ml;
-					}
-#endif
 					const int32_t len = rL[r] + rml[r];
 					const int32_t inc = wave_incl_scan(len);
 					rdst[r] = o_round + inc - len;  // literal destination
@@ -3260,20 +3242,40 @@ __device__ __forceinline__ int32_t decode_block_pp2(PpLds2& L, const uint8_t* __
 		bool pre = false, anyg = false;
 		{
 			int32_t o_round = ob0;
+			// both rounds parsed first, then the rare shapes, then placement
+			// (as decode_block)
+			bool fok[RMAX];
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r) {
 				rL[r] = rlit[r] = roff[r] = rml[r] = hml[r] = 0;
-				rbeg[r] = o_round;
-				if (64 * r < N) {
-					const int32_t idx = 64 * r + lane;
-					if (idx < N) {
+				fok[r] = true;
+				const int32_t idx = 64 * r + lane;
+				if (idx < N) {
+					Seq q;
+					fok[r] = parse_fast_try(S, base + int32_t(L.cst[w][idx]), n, q);
+					rL[r] = q.L;
+					rlit[r] = q.lit;
+					roff[r] = q.off;
+					rml[r] = q.ml;
+				}
+			}
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				if (__builtin_expect(__any(!fok[r]), 0)) {
+					if (!fok[r]) {
 						Seq q;
-						parse_fast(S, base + int32_t(L.cst[w][idx]), n, q);
+						parse_seq(S, base + int32_t(L.cst[w][64 * r + lane]), n, q);
 						rL[r] = q.L;
 						rlit[r] = q.lit;
 						roff[r] = q.off;
 						rml[r] = q.ml;
 					}
+				}
+			}
+#pragma unroll
+			for (int r = 0; r < RMAX; ++r) {
+				rbeg[r] = o_round;
+				if (64 * r < N) {
 					const int32_t len = rL[r] + rml[r];
 					const int32_t inc = wave_incl_scan(len);
 					rdst[r] = o_round + inc - len;
