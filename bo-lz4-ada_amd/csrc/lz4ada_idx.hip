@@ -1521,11 +1521,6 @@ __device__ __forceinline__ void load_chunk2(uintptr_t abase, int32_t c, uintptr_
 	}
 }
 
-#ifndef LZ4ADA_ZL_FILL
-#define LZ4ADA_ZL_FILL 1
-#endif
-constexpr bool ZL_FILL = LZ4ADA_ZL_FILL != 0;  // the zero plane zeroes a batch's span instead of its literal runs
-
 // Quirk D1 under the host's predicted round state (BLOCK_D1_ROUND: the
 // last round ended at OPH in [65536, 65542] and this block starts at round
 // position n1).  A match reading before the round start within 7 bytes of
@@ -1960,13 +1955,7 @@ __device__ __forceinline__ int32_t decode_block(DecLds& D, const uint8_t* __rest
 		// bytes that spill into its own match, rewritten in M, measured no
 		// faster.)
 		static_assert(RMAX == 2, "literal dealing pairs two rounds");
-		if (ZL && ZL_FILL) {
-			// the zero plane: every literal byte is 0, so the batch's whole
-			// span is zeroed (matches overwrite theirs in M) instead of
-			// dealing the runs
-			for (int32_t x = o_batch + 16 * lane; x < o_end; x += 64 * 16)
-				ostore(D, x, u32x4{ 0u, 0u, 0u, 0u }, min(16, o_end - x));
-		} else {
+		{
 #pragma unroll
 			for (int r = 0; r < RMAX; ++r)  // (rL = 0 also where a round has no sequence: n = 0)
 				ostore(D, rdst[r], ZL ? u32x4{ 0u, 0u, 0u, 0u } : fetch16(S, rL[r] > 0 ? rlit[r] : S.lo),
