@@ -152,26 +152,26 @@ def d1_matches(payload, n1, oph):
 
 def d1_emulable(payload, n1, oph):
     """Whether the index decoder emulates every D1 read of the block under
-    round state (n1, oph) (lz4ada_idx.hip d1_emulable): "yes" or "no".  A
-    read without literals copies the bytes after the previous match's source
-    (from HBM, or as a ring copy of its own when they are recent)."""
+    round state (n1, oph) (lz4ada_idx.hip d1_emulable).  A read without
+    literals copies the bytes after the previous match's source (from HBM,
+    or as a ring copy of its own when they are recent)."""
     for L, lit, m, off, ml, prev in d1_matches(payload, n1, oph):
         if n1 + m + ml > off:
-            return "no"
+            return False
         if L > 0:
             if lit + 8 * ((L - 1) // 8) + 8 > len(payload):
-                return "no"
+                return False
             continue
         if prev is None:
-            return "no"
+            return False
         pm, po, pml = prev
         f, pad = n1 + pm, (8 - pml % 8) % 8
         raw = f - po
         ok = (pml <= po and po - pml >= pad) if raw >= 0 else \
             (po - f >= pml and oph - po >= 8 and raw + pml + pad <= 0)
         if not ok:
-            return "no"
-    return "yes"
+            return False
+    return True
 
 
 def batch_starts(blocks, bmax, budget):
@@ -188,10 +188,9 @@ def batch_starts(blocks, bmax, budget):
     return set(starts)
 
 
-def d1_stops(blocks, bmax, budget=None):
-    """The blocks the linked bulk path may hand to the exact path for quirk
-    D1 (lz4ada_bulk_linked.cpp bulk_linked): (the first certain one or None,
-    whether an earlier one depends on the decoder's batch cuts).  The host
+def d1_stop(blocks, bmax, budget=None):
+    """The first block the linked bulk path hands to the exact path for
+    quirk D1 (lz4ada_bulk_linked.cpp bulk_linked), or None.  The host
     predicts each block's round state (Output_Pos / Output_Pos_History,
     lz4ada.adb:678-690, 785-787) with every block filling its slot; the
     index decoder emulates D1 under the prediction where d1_emulable says so
@@ -204,7 +203,6 @@ def d1_stops(blocks, bmax, budget=None):
     budget = budget or int(os.environ.get("LZ4ADA_LINKED_BATCH_BYTES", 2 << 30))
     starts = batch_starts(blocks, bmax, budget)
     opos = oph = po = ph = 0
-    maybe = False
     for k, (comp, raw) in enumerate(blocks):
         if k in starts:  # each batch predicts from the real state at its start
             po, ph = opos, oph
@@ -214,41 +212,26 @@ def d1_stops(blocks, bmax, budget=None):
             po = 0
         risk = any(off > q and off >= 65529 for q, off in matches(comp))
         in_d1, pd1 = 65536 <= oph <= 65542, 65536 <= ph <= 65542
-        emu = d1_emulable(comp, po, ph) if pd1 else "no"
-        if risk:
-            exact = (po, ph) == (opos, oph)
-            if in_d1 and not (emu == "yes" and exact) and not (emu == "maybe" and exact):
-                return k, maybe
-            if in_d1 and emu == "maybe":
-                maybe = True
-            if not in_d1 and emu == "yes":
-                return k, maybe
-            if not in_d1 and emu == "maybe":
-                maybe = True
+        emu = pd1 and d1_emulable(comp, po, ph)
+        if risk and (not (emu and (po, ph) == (opos, oph)) if in_d1 else emu):
+            return k
         opos += len(raw)
         po += min(bmax, 255 * len(comp) + 64)
         if opos >= 65536:
             oph = opos
         if po >= 65536:
             ph = po
-    return None, maybe
-
-
-def d1_stop(blocks, bmax, budget=None):
-    return d1_stops(blocks, bmax, budget)[0]
+    return None
 
 
 def want_path(blocks, bmax, ok=True):
-    """The paths lz4ada_last_path() may report: the linked bulk path takes
-    the frame; at a block quirk D1 sends to the exact path, that path
-    resumes and finishes it.  ok=False (the reference raises at the end,
-    e.g. a content checksum its D1 bytes do not match): a bulk pass that
-    reaches the end hands the whole frame to the exact path for the
-    exception."""
-    stop, maybe = d1_stops(blocks, bmax)
+    """The path lz4ada_last_path() reports: the linked bulk path takes the
+    frame; at a block quirk D1 sends to the exact path, that path resumes
+    and finishes it.  ok=False (the reference raises at the end, e.g. a
+    content checksum its D1 bytes do not match): a bulk pass that reaches
+    the end hands the whole frame to the exact path for the exception."""
     L, E = lz4ada.PATH_LINKED, lz4ada.PATH_EXACT
-    done = L if ok else E
-    return {L | E} if stop is not None else ({done, L | E} if maybe else {done})
+    return L | E if d1_stop(blocks, bmax) is not None else (L if ok else E)
 
 
 # ------------------------------------------------------------ linked frames
@@ -270,7 +253,7 @@ def test_linked_frame_bulk(kind, bmax):
         with pytest.raises(lz4ada.LZ4AdaError) as ei:
             lz4ada.decode_frame(frame)
         assert str(ei.value) == O.exception_information(st, msg)
-    assert lz4ada.last_path() in want_path(blocks, bmax, st == O.OK)
+    assert lz4ada.last_path() == want_path(blocks, bmax, st == O.OK)
 
 
 def test_linked_frame_mixed_block_sizes():
@@ -283,7 +266,7 @@ def test_linked_frame_mixed_block_sizes():
     assert st == O.OK and ref == raw, msg
     out, _ = lz4ada.decode_frame(frame)
     assert out == raw
-    assert lz4ada.last_path() in want_path(blocks, 256 * KiB)
+    assert lz4ada.last_path() == want_path(blocks, 256 * KiB)
 
 
 @pytest.mark.parametrize("batch", [None, 300 * KiB, 1])
@@ -318,14 +301,14 @@ def test_linked_word_modes(kind, words, batch, env):
     lens = [65536, 70001, 100, 65535, 131075, 3, 65536, 200001, 4097]
     frame, raw, blocks = linked_frame(lz4ada.GEN_KINDS[kind], lens, 256 * KiB, seed=17)
     st, _ = same_as_oracle(frame)
-    assert lz4ada.last_path() in want_path(blocks, 256 * KiB, st == O.OK)
+    assert lz4ada.last_path() == want_path(blocks, 256 * KiB, st == O.OK)
 
 
 def test_linked_small_batches_64k(env):
     env("LZ4ADA_LINKED_BATCH_BYTES", str(200 * KiB))
     frame, raw, blocks = linked_frame(lz4ada.GEN_MIXED, [65536] * 9 + [4000], 64 * KiB, seed=3)
     st, _ = same_as_oracle(frame)
-    assert lz4ada.last_path() in want_path(blocks, 64 * KiB, st == O.OK)
+    assert lz4ada.last_path() == want_path(blocks, 64 * KiB, st == O.OK)
 
 
 def d1_frame(content_cksum):
@@ -366,7 +349,7 @@ def test_d1_uniform_offsets_64k_frame():
     assert st == O.OK, msg
     out, _ = lz4ada.decode_frame(frame)
     assert out == ref
-    assert lz4ada.last_path() in want_path(blocks, 64 * KiB)
+    assert lz4ada.last_path() == want_path(blocks, 64 * KiB)
 
 
 @pytest.mark.parametrize("lit_len,pof,pml,off", [(16, 16, 4, 65533), (16, 16, 9, 65535), (3, 1000, 10, 65534),
@@ -385,7 +368,7 @@ def test_d1_without_literals_in_bulk(lit_len, pof, pml, off):
     info, descs = lz4ada.frame_index(frame)
     blocks = [(frame[d.in_off:d.in_off + d.in_len], b"\0" * (65536 if k == 0 else len(ref) - 65536))
               for k, d in enumerate(descs[:info.nblocks])]
-    assert lz4ada.last_path() in want_path(blocks, 64 * KiB)
+    assert lz4ada.last_path() == want_path(blocks, 64 * KiB)
     assert lz4ada.last_path() == lz4ada.PATH_LINKED
 
 
