@@ -954,15 +954,15 @@ struct alignas(16) DecLds {
 static_assert(sizeof(DecLds) <= 20480, "8 waves per CU: at most 20 KiB of LDS per wave");
 
 // The output window and per-wave scratch of an LDS layout: DecLds (one
-// wave per block) holds them directly; a two-wave block's view (W2, below)
-// picks its wave's scratch.
+// wave per block) holds them directly; a k_decode_pp2 wave's view (WP2,
+// below) picks its wave's scratch.
 __device__ __forceinline__ uint8_t* oring_of(DecLds& D) { return D.oring; }
 __device__ __forceinline__ const uint8_t* oring_of(const DecLds& D) { return D.oring; }
 __device__ __forceinline__ uint8_t* own_of(DecLds& D) { return D.own; }
 __device__ __forceinline__ uint64_t* ldesc_of(DecLds& D) { return D.ldesc; }
 // Layouts with junk bytes and the pattern selectors (the one-wave decoder):
 // branch-free exact stores (lds_store_bf) and period patterns by v_perm
-// (pattern_perm); the two-wave layouts keep the branching forms.
+// (pattern_perm); the two-wave layout keeps the branching forms.
 template <class LD>
 struct lds_fast {
 	static constexpr bool value = false;
@@ -2242,25 +2242,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 }
 
 // ============================================================ two waves
-// k_decode_idx2: the fused decode of k_decode_idx with TWO waves per block
-// (one 128-lane workgroup), so the 2048 blocks of the bench put four waves
-// on every SIMD instead of two.  Each wave of k_decode_idx is latency-bound
-// (one block's serial chain: a second wave on a SIMD costs the first one
-// nothing), and a block cannot be cut into independent output
-// ranges (a range's matches reach the previous range's output, and on this
-// data the dependence spreads through most of the range: tools/taint_sim.cpp),
-// so the two waves share each step of the chain instead:
-//  * pass 1: 128 lanes walk one 16 KiB chunk, 128 bytes each; wave 0's
-//    lane 0 enters at the exact chain position, wave 1's lane 0 at its
-//    lead-in guess until wave 0's exit is known (one exchange per chunk);
-//  * pass 2: a batch's sub-segments are split at a sequence count -- wave 0
-//    parses, copies literals and loads HBM-sourced matches of its <= 64
-//    sequences, wave 1 of the next <= 64, in parallel; their output offsets
-//    come from pass 1's records.  Ring-sourced matches of wave 1 that read
-//    wave 0's ring-match output (or a match of its own that does) wait for
-//    wave 0; the rest run beside it.  Three barriers per batch.
-// LDS is shared (under 20 KiB per block, so 8 blocks = 16 waves per CU) and
-// each wave fits in 128 VGPRs.
+// Pass 1 by the two waves of a 128-lane workgroup (k_decode_pp2's): 128
+// lanes walk one 16 KiB chunk, 128 bytes each; wave 0's lane 0 enters at
+// the exact chain position, wave 1's lane 0 at its lead-in guess until wave
+// 0's exit is known (one exchange per chunk).  (Round 4's k_decode_idx2,
+// which also split each pass-2 batch between the two waves, was retired in
+// round 6: k_decode_pp2 pipelining whole batches replaced it where two
+// waves per block pay, docs/DESIGN_LOG.md §3.)
 
 constexpr int SEG2 = 128;          // pass-1 segment per lane: 128 lanes per 16 KiB chunk
 constexpr int NSUB2 = SEG2 / SUB;  // records per segment
@@ -2440,490 +2428,6 @@ __device__ __forceinline__ void index_block2(IdxLds2& X, const uint8_t* __restri
 	if (tid == 0)
 		status[b].code = bad ? (sparse ? DS_SPARSE : DS_RETRY) : DS_OK;
 }
-
-struct alignas(16) DecLds2 {
-	uint8_t ring[RING + 16];  // staged input: 4 chunks of 2 KiB (+ mirror); each wave stages half
-	uint8_t oring[ORING];     // output window, shared
-	uint64_t rrec[4 * 64];    // pass-1 records of the staged chunks (wave 0 loads them)
-	uint64_t ldesc[2][64];    // per wave: run / match descriptors of its dealt pieces
-	uint16_t cst[2][64];      // per wave: its sequence starts, in order
-	uint8_t own[2][64];       // per wave: piece owners
-	int32_t xc[2][4];         // per wave: bad; wave 0: its ring-match span [lo, hi)
-};
-
-// One wave's view: the shared window, its own scratch.
-struct W2 {
-	DecLds2& L;
-	int32_t w;
-};
-__device__ __forceinline__ uint8_t* oring_of(W2& V) { return V.L.oring; }
-__device__ __forceinline__ const uint8_t* oring_of(const W2& V) { return V.L.oring; }
-__device__ __forceinline__ uint8_t* own_of(W2& V) { return V.L.own[V.w]; }
-__device__ __forceinline__ uint64_t* ldesc_of(W2& V) { return V.L.ldesc[V.w]; }
-
-// ring_pieces for one round (a wave's 64 sequences).
-template <class LD>
-__device__ __forceinline__ int32_t ring_pieces1(LD& D, int32_t mdst, int32_t off, int32_t ml,
-                                                int32_t o_batch)
-{
-	int32_t steps = 0;
-	const int32_t lane = int32_t(lane_id());
-	const int32_t np = match_pieces(off, ml);
-	const int32_t inc = wave_incl_scan(np);
-	const int32_t tot = __shfl(inc, 63);
-	uint64_t* ldesc = ldesc_of(D);
-	ldesc[lane] = uint64_t(uint16_t(mdst - o_batch)) | (uint64_t(uint16_t(off)) << 16) |
-	              (uint64_t(uint16_t(ml)) << 32) | (uint64_t(uint16_t(inc - np)) << 48);
-	for (int32_t t0 = 0; t0 < tot; t0 += 64) {
-		const int32_t t = t0 + lane;
-		const bool act = t < tot;
-		const int32_t lo = min(chunk_owner(D, inc, np, t0), 63);
-		const uint64_t dd = ldesc[lo];
-		const int32_t od = o_batch + int32_t(dd & 0xffffu);
-		const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
-		const int32_t k = t - int32_t(dd >> 48);
-		const bool opat = ooff < 16 && ooff < oml;
-		const int32_t ostp = opat ? pattern_step(ooff) : 16;
-		const bool wide = !opat && oml > ooff;
-		const int32_t pd = od + k * ostp;
-		const int32_t pn = min(16, oml - k * ostp);
-		const int32_t s_lo = (opat || wide) ? od - ooff : od - ooff + 16 * k;
-		const int32_t s_hi = (opat || wide) ? od : s_lo + pn;
-		const int32_t pe = act ? pd + pn : INT32_MAX, ps = act ? pd : INT32_MAX;
-		uint64_t dep = 0;
-		if (!__all(!act || s_hi <= __shfl(ps, 0))) {
-			int32_t j1 = 0, c2 = 0;
-#pragma unroll
-			for (int st = 32; st >= 1; st >>= 1) {
-				if (__shfl(pe, j1 + st - 1) <= s_lo)
-					j1 += st;
-				if (__shfl(ps, c2 + st - 1) < s_hi)
-					c2 += st;
-			}
-			const int32_t j2 = min(c2 - 1, lane - 1);
-			if (act && j1 <= j2)
-				dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
-		}
-		bool pend = act;
-		for (;;) {
-			const uint64_t pm = __ballot(pend);
-			if (pm == 0)
-				break;
-			const bool ready = pend && (dep & pm) == 0;
-			if (ready) {
-				int32_t rem = 0;
-				if (wide)
-					div_small(16 * k, ooff, rem);
-				const int32_t a1 = opat ? od - ooff : (wide ? od - ooff + rem : s_lo);
-				u32x4 v = oload16(D, a1);
-				if (wide && ooff - rem < 16)
-					v = merge_at(v, oload16(D, a1 - ooff), ooff - rem);
-				if (opat) {
-					int32_t sstp;
-					make_pattern16(uint64_t(v.x) | (uint64_t(v.y) << 32),
-					               uint64_t(v.z) | (uint64_t(v.w) << 32), ooff, v, sstp);
-				}
-				ostore(D, pd, v, pn);
-			}
-			pend = pend && !ready;
-			wave_lds_fence();
-			++steps;
-		}
-	}
-	return steps;
-}
-
-// A wave's ring-sourced matches (ml = 0: none): dealt pieces when one is
-// long, else one lane each.
-template <class LD>
-__device__ __forceinline__ void ring_round(LD& D, int32_t mdst, int32_t off, int32_t ml, int32_t rbeg,
-                                           int32_t L, int32_t o_batch)
-{
-	if (__any(ml > RING_LANE_MAX))
-		ring_pieces1(D, mdst, off, ml, o_batch);
-	else
-		ring_lanes(D, mdst, off, ml, rbeg, L);
-}
-
-// Pass 2 of block b by both waves (decode_block's rules, independent blocks).
-__device__ __forceinline__ void decode_block2(DecLds2& L, const uint8_t* __restrict__ frame,
-                                              uint64_t frame_len,
-                                              const lz4ada_block_desc* __restrict__ desc, uint32_t b,
-                                              const uint8_t* __restrict__ tab_all,
-                                              uint8_t* __restrict__ out,
-                                              lz4ada_block_status* __restrict__ status)
-{
-	const int32_t tid = int32_t(threadIdx.x), w = tid >> 6, lane = tid & 63;
-	W2 V{ L, w };
-	const lz4ada_block_desc d = desc[b];
-	if (status[b].code != DS_OK)
-		return;  // pass 1 declined it (its status says so)
-	cg8* in = gptr(frame) + d.in_off;
-	g8* ob = gptr(out) + d.out_off;
-	const int32_t n = int32_t(d.in_len);
-	const int32_t cap = int32_t(d.out_cap);
-	const uintptr_t lim = reinterpret_cast<uintptr_t>(frame) + frame_len;
-	const uintptr_t olim = reinterpret_cast<uintptr_t>(ob) + uintptr_t(cap);
-
-	if (d.flags & LZ4ADA_BLOCK_STORED) {
-		int32_t code = DS_OK;
-		if (n > cap) {
-			code = DS_OUT_OVERFLOW;
-		} else {  // each wave copies half
-			Src S0;
-			S0.in = in;
-			S0.lim = lim;
-			const int32_t mid = (n >> 1) & ~1023;
-			const int32_t c0 = w == 0 ? 0 : mid, c1 = w == 0 ? mid : n;
-			if (d.flags & LZ4ADA_BLOCK_HAS_CKSUM)
-				wave_literal<0>(ob, c0, S0, c0, c1 - c0);
-			else
-				wave_literal<LZ4ADA_STORED_NT>(ob, c0, S0, c0, c1 - c0);
-		}
-		if (tid == 0) {
-			status[b].code = code;
-			status[b].aux = 0;
-			status[b].detail = 0;
-			status[b].err_out_pos = 0;
-			status[b].out_len = code == DS_OK ? uint32_t(n) : 0u;
-		}
-		return;
-	}
-
-	const int32_t mis = int32_t(reinterpret_cast<uintptr_t>(in) & 15u);
-	const uint64_t* tab = reinterpret_cast<const uint64_t*>(tab_all) + (((d.in_off >> 8) + b) << 3);
-	const int32_t nsub = (n + SUB - 1) / SUB;
-	const uintptr_t abase = reinterpret_cast<uintptr_t>(in) - uintptr_t(mis);
-
-	Src S;
-	S.lds = L.ring;
-	S.mask = RING - 1;
-	S.mis = mis;
-	S.in = in;
-	S.lim = lim;
-
-	// this wave's half (1 KiB) of input chunk c, and (wave 0) its 64 records
-	auto load_half = [&](int32_t c) -> u32x4 {
-		const uintptr_t g = abase + uintptr_t(c) * BATCH + uintptr_t(1024 * w + 16 * lane);
-		u32x4 v;
-		if (abase + uintptr_t(c + 1) * BATCH <= lim)
-			__builtin_memcpy(&v, reinterpret_cast<cg8*>(g), 16);
-		else
-			v = gload16(g, lim);
-		return v;
-	};
-	auto load_rec = [&](int32_t c) -> uint64_t {
-		const int32_t k = 64 * c + lane;
-		return (w == 0 && k < nsub) ? __builtin_nontemporal_load(tab + k) : 0;
-	};
-	int32_t hi = 0;
-	u32x4 pf = load_half(0);
-	uint64_t pr = load_rec(0);
-	vm_wait();
-
-	int32_t o_batch = 0;
-	bool bad = false;
-	for (int32_t k0 = 0; k0 < nsub && !bad;) {
-		// only this wave's last flush may still be in flight: what the other
-		// wave reads from HBM (sources two batches old) has landed
-		asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FLUSH_ST) : "memory");
-		const int32_t cf = (k0 * SUB + mis) / BATCH;
-		while (hi < cf + 3) {  // never a chunk the previous batch still reads
-			const uint32_t a = uint32_t(hi * BATCH) & (RING - 1);
-			*reinterpret_cast<u32x4*>(&L.ring[a + 1024 * w + 16 * lane]) = pf;
-			if (a == 0 && tid == 0)
-				*reinterpret_cast<u32x4*>(&L.ring[RING]) = pf;
-			if (w == 0)
-				L.rrec[64 * (hi & 3) + lane] = pr;
-			++hi;
-			pf = load_half(hi);
-			pr = load_rec(hi);
-		}
-		__syncthreads();  // barrier 0: staged input visible; the previous batch done
-		S.lo = max(hi - 4, 0) * BATCH - mis;
-		S.hi = hi * BATCH - mis;
-
-		// the cut, computed alike by both waves: wave 0 takes the first
-		// sub-segments (<= 64 sequences), wave 1 the next ones (<= 64)
-		const int32_t k = k0 + lane;
-		const int32_t sub_s = k * SUB;
-		const int32_t sub_end = min(sub_s + SUB, n);
-		const uint64_t rec = (k < nsub) ? L.rrec[k & 255] : 0;
-		uint32_t bm = uint32_t(rec);
-		const int32_t cnt = int32_t(min(uint32_t(rec >> 32), 1u << 24));
-		const int32_t nseq = __popc(bm);
-		const int32_t p0 = bm ? sub_s + __builtin_ctz(bm) : n;
-		const int32_t incl = wave_incl_scan(cnt);
-		const int32_t incl_s = wave_incl_scan(nseq);
-		const int32_t mA = __popcll(__ballot(incl <= OW && incl_s <= 64));
-		const int32_t sA = mA ? __shfl(incl_s, mA - 1) : 0;
-		const int32_t oA = mA ? __shfl(incl, mA - 1) : 0;
-		const int32_t m = __popcll(__ballot(incl <= OW && incl_s - sA <= 64));
-
-		if (m == 0) {
-			// oversized (batch_global): wave 0 alone, straight to HBM
-			const int32_t total = __shfl(incl, 63);
-			if (o_batch + total > cap) {
-				bad = true;
-				break;
-			}
-			vm_wait();  // both waves' flushes landed (the batch reads them back)
-			__syncthreads();
-			if (w == 0) {
-				const int32_t a0 = o_batch & ~15;
-				if (lane == 0 && o_batch > a0)
-					gstore_n(ob + a0, *reinterpret_cast<const u32x4*>(&L.oring[a0 & OMASK]), o_batch - a0);
-				vm_wait();
-				const bool ok = batch_global(S, ob, olim, p0, sub_end, n, o_batch + incl - cnt, o_batch, 0);
-				vm_wait();
-				const int32_t ob2 = o_batch + total;
-				const int32_t x0 = max(ob2 - ORING + 16, 0) & ~15;
-				for (int32_t x = x0 + 16 * lane; x < ob2 + 15; x += 64 * 16)
-					*reinterpret_cast<u32x4*>(&L.oring[uint32_t(x) & OMASK]) =
-					    gload16(reinterpret_cast<uintptr_t>(ob) + uintptr_t(intptr_t(x)), olim);
-				__builtin_amdgcn_s_waitcnt(0x0F70);
-				if (lane == 0)
-					L.xc[0][0] = ok ? 0 : 1;
-			}
-			wave_lds_fence();
-			__syncthreads();
-			if (L.xc[0][0]) {
-				bad = true;
-				break;
-			}
-			o_batch += total;
-			k0 += 64;
-			continue;
-		}
-
-		const int32_t o_end = o_batch + __shfl(incl, m - 1);
-		if (o_end > cap) {
-			bad = true;
-			break;
-		}
-		const int32_t base = k0 * SUB;
-		const int32_t lo_l = w ? mA : 0, hi_l = w ? m : mA;
-		if (lane >= lo_l && lane < hi_l) {
-			int32_t e = incl_s - nseq - (w ? sA : 0);
-			const uint16_t rel = uint16_t(sub_s - base);
-			for (; bm; bm &= bm - 1)
-				L.cst[w][e++] = uint16_t(rel + __builtin_ctz(bm));
-		}
-		wave_lds_fence();
-		const int32_t N = w ? __shfl(incl_s, m - 1) - sA : sA;
-		const int32_t glo = o_batch - OW - 16;
-		const int32_t ow0 = o_batch + (w ? oA : 0);  // this wave's first output byte
-
-		// P: this wave's sequences, placed by a prefix sum
-		int32_t rL = 0, rlit = 0, roff = 0, rml = 0;
-		if (lane < N) {
-			Seq q;
-			parse_fast(S, base + int32_t(L.cst[w][lane]), n, q);
-			rL = q.L;
-			rlit = q.lit;
-			roff = q.off;
-			rml = q.ml;
-		}
-		const int32_t len = rL + rml;
-		const int32_t inc0 = wave_incl_scan(len);
-		const int32_t rdst = ow0 + inc0 - len;
-		const int32_t mdst = rdst + rL;
-		// a reference before the block start (D2): the block is declined
-		const bool mybad = __any(rml > 0 && roff > mdst);
-		if (mybad)
-			rL = rml = 0;
-		const int32_t src = mdst - roff;
-		const bool hbm = rml > 0 && src < glo;
-
-		// HBM-sourced matches: first piece in its own lane, the rest dealt
-		u32x4 vg = u32x4{ 0u, 0u, 0u, 0u }, vr = u32x4{ 0u, 0u, 0u, 0u };
-		int32_t rpd = 0, rpn = 0, rtot = 0;
-		if (__any(hbm)) {
-			if (hbm)
-				__builtin_memcpy(&vg, ob + src, 16);
-			const int32_t nc = hbm ? max(((rml + 15) >> 4) - 1, 0) : 0;
-			if (__any(nc > 0)) {
-				const int32_t incc = wave_incl_scan(nc);
-				rtot = __shfl(incc, 63);
-				uint64_t* ldesc = ldesc_of(V);
-				ldesc[lane] = uint64_t(uint16_t(mdst - o_batch)) | (uint64_t(uint16_t(roff)) << 16) |
-				              (uint64_t(uint16_t(rml)) << 32) | (uint64_t(uint16_t(incc - nc)) << 48);
-				const int32_t lo = min(chunk_owner(V, incc, nc, 0), 63);
-				const uint64_t dd = ldesc[lo];
-				const int32_t od = o_batch + int32_t(dd & 0xffffu);
-				const int32_t ooff = int32_t((dd >> 16) & 0xffffu), oml = int32_t((dd >> 32) & 0xffffu);
-				const int32_t kk = 1 + lane - int32_t(dd >> 48);
-				if (lane < rtot) {
-					rpd = od + 16 * kk;
-					rpn = min(16, oml - 16 * kk);
-					__builtin_memcpy(&vr, ob + (od - ooff) + 16 * kk, 16);
-				}
-				wave_lds_fence();
-			}
-		}
-
-		// L: literals, input ring -> output window (first piece in-lane)
-		if (rL > 0)
-			ostore(V, rdst, fetch16(S, rlit), min(16, rL));
-		{
-			const int32_t ncl = rL > 16 ? (rL - 1) >> 4 : 0;
-			if (__any(ncl > 0)) {
-				const int32_t incl2 = wave_incl_scan(ncl);
-				const int32_t tot = __shfl(incl2, 63);
-				uint64_t* ldesc = ldesc_of(V);
-				ldesc[lane] = uint64_t(uint16_t(rlit - base)) | (uint64_t(uint16_t(rdst - o_batch)) << 16) |
-				              (uint64_t(uint16_t(rL)) << 32) | (uint64_t(uint16_t(incl2 - ncl)) << 48);
-				for (int32_t t0 = 0; t0 < tot; t0 += 64) {
-					const int32_t t = t0 + lane;
-					const int32_t lo = min(chunk_owner(V, incl2, ncl, t0), 63);
-					const uint64_t dd = ldesc[lo];
-					const int32_t lit = base + int32_t(dd & 0xffffu);
-					const int32_t dst = o_batch + int32_t((dd >> 16) & 0xffffu);
-					const int32_t Lx = int32_t((dd >> 32) & 0xffffu);
-					const int32_t kk = 1 + t - int32_t(dd >> 48);
-					if (t < tot)
-						ostore(V, dst + 16 * kk, fetch16(S, lit + 16 * kk), min(16, Lx - 16 * kk));
-				}
-			}
-		}
-		wave_lds_fence();
-
-		// M, HBM-sourced stores (their sources are in HBM: no order among them)
-		__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-		if (rpn > 0)
-			ostore(V, rpd, vr, rpn);
-		if (hbm)
-			ostore(V, mdst, vg, min(16, rml));
-		if (rtot > 64) {  // rare: more than 64 dealt pieces
-			const int32_t nc = hbm ? max(((rml + 15) >> 4) - 1, 0) : 0;
-			const int32_t inc = wave_incl_scan(nc);
-			for (int32_t t0 = 64; t0 < rtot; t0 += 64) {
-				const int32_t t = t0 + lane;
-				const int32_t lo = piece_owner(inc, t);
-				const int32_t kk = 1 + t - (__shfl(inc, lo) - __shfl(nc, lo));
-				const int32_t osrc = __shfl(mdst - roff, lo), odst = __shfl(mdst, lo);
-				const int32_t oml = __shfl(rml, lo);
-				if (t < rtot) {
-					u32x4 v;
-					__builtin_memcpy(&v, ob + osrc + 16 * kk, 16);
-					ostore(V, odst + 16 * kk, v, min(16, oml - 16 * kk));
-				}
-			}
-			__builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-		}
-		const int32_t lring = (rml > 0 && !hbm) ? rml : 0;
-		if (w == 0) {  // where wave 0's ring-sourced matches write: [lo, hi)
-			constexpr int32_t BIG = 1 << 30;
-			const int32_t mlo = __shfl(wave_incl_max(lring ? BIG - mdst : 0), 63);
-			const int32_t mhi = __shfl(wave_incl_max(lring ? mdst + lring : 0), 63);
-			if (lane == 0) {
-				L.xc[0][1] = mlo ? BIG - mlo : BIG;
-				L.xc[0][2] = mhi;
-			}
-		}
-		if (lane == 0)
-			L.xc[w][0] = mybad ? 1 : 0;
-		wave_lds_fence();
-		__syncthreads();  // barrier 1: literals and HBM-sourced bytes of both waves in place
-		if (L.xc[0][0] | L.xc[1][0]) {
-			bad = true;
-			break;
-		}
-		const int32_t u0 = o_batch >> 4, uA = (o_batch + oA) >> 4, u1 = o_end >> 4;
-		auto flush = [&](int32_t ua, int32_t ub) {  // FLUSH_ST store instructions, always
-#pragma unroll
-			for (int i = 0; i < FLUSH_ST; ++i) {
-				const int32_t u = ua + lane + 64 * i;
-				if (u < ub)
-					*reinterpret_cast<GLOBAL u32x4*>(ob + (u << 4)) =
-					    *reinterpret_cast<const u32x4*>(&L.oring[(u << 4) & OMASK]);
-			}
-		};
-		bool dfr = false;
-		if (w == 0) {
-			ring_round(V, mdst, roff, lring, ow0, rL, o_batch);
-			wave_lds_fence();
-			flush(u0, uA);  // wave 1 never writes below its first byte
-		} else {
-			// matches reading wave 0's ring-match output wait for it, and so
-			// does every match reading one of those (within this wave)
-			const int32_t alo = L.xc[0][1], ahi = L.xc[0][2];
-			const int32_t send = src + min(roff, lring);
-			dfr = lring > 0 && src < ahi && send > alo;
-			if (__any(dfr)) {
-				const int32_t mend = mdst + lring;
-				int32_t j1 = 0, c2 = 0;
-#pragma unroll
-				for (int st = 32; st >= 1; st >>= 1) {
-					if (__shfl(mend, j1 + st - 1) <= src)
-						j1 += st;
-					if (__shfl(mdst, c2 + st - 1) < send)
-						c2 += st;
-				}
-				const int32_t j2 = min(c2 - 1, lane - 1);
-				uint64_t dep = 0;
-				if (lring > 0 && j1 <= j2)
-					dep = (j2 == 63 ? ~uint64_t(0) : ((uint64_t(2) << j2) - 1)) & ~((uint64_t(1) << j1) - 1);
-				uint64_t D = __ballot(dfr);
-				for (;;) {
-					dfr = lring > 0 && (dfr || (dep & D) != 0);
-					const uint64_t D2 = __ballot(dfr);
-					if (D2 == D)
-						break;
-					D = D2;
-				}
-			}
-			ring_round(V, mdst, roff, dfr ? 0 : lring, ow0, rL, o_batch);
-		}
-		wave_lds_fence();
-		__syncthreads();  // barrier 2: wave 0's matches in place
-		if (w == 1) {
-			if (__any(dfr))
-				ring_round(V, mdst, roff, dfr ? lring : 0, ow0, rL, o_batch);
-			wave_lds_fence();
-			flush(uA, u1);
-		}
-		o_batch = o_end;
-		k0 += m;
-	}
-	__syncthreads();
-	if (!bad && tid == 0 && (o_batch & 15))  // last partial unit
-		gstore_n(ob + (o_batch & ~15), *reinterpret_cast<const u32x4*>(&L.oring[(o_batch & ~15) & OMASK]),
-		         o_batch & 15);
-	if (tid == 0) {
-		if (bad) {
-			status[b].code = DS_RETRY;
-		} else {
-			status[b].code = DS_OK;
-			status[b].aux = 0;
-			status[b].detail = 0;
-			status[b].err_out_pos = 0;
-			status[b].out_len = uint32_t(o_batch);
-		}
-	}
-}
-
-// Independent blocks, both passes, two waves per block.  Pinned to four
-// waves per SIMD (128 VGPRs): LDS allows 8 blocks = 16 waves per CU.
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_idx2(
-        const uint8_t* __restrict__ frame, uint64_t frame_len, const lz4ada_block_desc* __restrict__ desc,
-        uint32_t nblocks, uint8_t* __restrict__ tab_all, uint8_t* __restrict__ out,
-        lz4ada_block_status* __restrict__ status)
-{
-	__shared__ union {
-		DecLds2 d;
-		IdxLds2 x;
-	} U;
-	if (blockIdx.x >= nblocks)
-		return;
-	index_block2(U.x, frame, frame_len, desc, blockIdx.x, tab_all, status);
-	vm_wait();
-	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-	__syncthreads();
-	decode_block2(U.d, frame, frame_len, desc, blockIdx.x, tab_all, out, status);
-}
-
-
 
 // ============================================================ pipelined pair
 // k_decode_pp2 (round 5): two waves per block that pipeline consecutive
@@ -3614,13 +3118,9 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
 		return hipGetLastError();
 	}
-	if (mode == 5) {  // both passes, two waves per block pipelining batches (k_decode_pp2)
+	if (mode == 5 || mode == 4) {  // both passes, two waves per block pipelining batches (k_decode_pp2;
+		                           // 4: round 4's k_decode_idx2, retired -- its callers get pp2)
 		hipLaunchKernelGGL(idx::k_decode_pp2, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
-		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
-		return hipGetLastError();
-	}
-	if (mode == 4) {  // both passes, two waves per block (k_decode_idx2)
-		hipLaunchKernelGGL(idx::k_decode_idx2, dim3(nblocks), dim3(128), 0, stream, d_frame, frame_len,
 		                   d_desc, nblocks, const_cast<uint8_t*>(d_tab), d_out, d_status);
 		return hipGetLastError();
 	}
@@ -3630,18 +3130,16 @@ hipError_t launch_decode_idx_tab(const uint8_t* d_frame, uint64_t frame_len,
 }
 
 // The fused launch for independent blocks.  One wave per block
-// (k_decode_idx, mode 3) while the blocks fill the chip's SIMDs twice;
-// two waves per block (k_decode_idx2, mode 4) for at most one block per
-// SIMD, where the second wave has a SIMD of its own (measured, DESIGN §4:
-// 1024 x 4 MiB mixed 12.05 -> 11.28 ms, but 2048 x 4 MiB 13.29 -> 13.98 ms:
-// each block's chain is latency-bound, so splitting a batch between two
-// waves shortens it little, and four waves per SIMD contend).
-// LZ4ADA_IDX_WAVES=1 / 2 forces one or the other.
+// (k_decode_idx, mode 3) while the blocks fill the chip's SIMDs twice; two
+// waves per block pipelining batches (k_decode_pp2, mode 5) for at most 4
+// blocks per CU (measured, docs/DESIGN_LOG.md §3: 1,024 x 4 MiB mixed 12.0
+// -> 8.7 ms, but at 2,048 blocks 13.3 -> 18.0 ms).  LZ4ADA_IDX_WAVES=1 / p
+// (or 2, which meant the retired k_decode_idx2) forces one or the other.
 int idx_fused_mode(uint32_t nblocks)
 {
 	static const int forced = [] {
 		const char* e = getenv("LZ4ADA_IDX_WAVES");
-		return e ? (e[0] == '1' ? 3 : (e[0] == '2' ? 4 : (e[0] == 'p' ? 5 : 0))) : 0;
+		return e ? (e[0] == '1' ? 3 : ((e[0] == '2' || e[0] == 'p') ? 5 : 0)) : 0;
 	}();
 	if (forced)
 		return forced;
@@ -3654,7 +3152,7 @@ int idx_fused_mode(uint32_t nblocks)
 const char* idx_fused_kernel_name(uint32_t nblocks)
 {
 	const int m = idx_fused_mode(nblocks);
-	return m == 5 ? "k_decode_pp2" : (m == 4 ? "k_decode_idx2" : "k_decode_idx");
+	return m == 5 ? "k_decode_pp2" : "k_decode_idx";
 }
 
 hipError_t launch_decode_idx(const uint8_t* d_frame, uint64_t frame_len,

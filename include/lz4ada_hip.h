@@ -250,11 +250,12 @@ int lz4ada_launch_decode(const void *d_frame, uint64_t frame_len,
  * declines keep status code 10 (retry). */
 #define LZ4ADA_DECODE_IDX_SPARSE 6
 /* The fused index decoder alone with one wave per block (k_decode_idx) or
- * two (k_decode_idx2); declined blocks keep status code 10.  The default of
- * LZ4ADA_DECODE_IDX / _ALONE picks by launch size: k_decode_pp2 for at most
- * 4x the CU count in blocks, k_decode_idx above; LZ4ADA_IDX_WAVES=1 / 2 / p
- * forces k_decode_idx / k_decode_idx2 / k_decode_pp2
- * (lz4ada_bulk_decoder_kernel() names the one a launch uses). */
+ * two pipelining batches (k_decode_pp2; _IDX2_ALONE named round 4's
+ * k_decode_idx2, retired in round 6, and now runs k_decode_pp2); declined
+ * blocks keep status code 10.  The default of LZ4ADA_DECODE_IDX / _ALONE
+ * picks by launch size: k_decode_pp2 for at most 4x the CU count in
+ * blocks, k_decode_idx above; LZ4ADA_IDX_WAVES=1 / p forces k_decode_idx /
+ * k_decode_pp2 (lz4ada_bulk_decoder_kernel() names the one a launch uses). */
 #define LZ4ADA_DECODE_IDX1_ALONE 7
 #define LZ4ADA_DECODE_IDX2_ALONE 8
 /* The pipelined two-wave decoder (k_decode_pp2: two waves per block taking

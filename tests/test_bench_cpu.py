@@ -83,6 +83,6 @@ def test_kernel_code_hash_guards_traffic_figure():
     h = bench.kernel_code_hash("k_decode_idx")
     assert h is not None and len(h) == 16
     assert h == bench.kernel_code_hash("k_decode_idx")
-    assert h != bench.kernel_code_hash("k_decode_idx2")  # not a prefix match
+    assert h != bench.kernel_code_hash("k_decode_idx_lk")  # not a prefix match
     assert bench.kernel_code_hash("no_such_kernel") is None
     assert bench.kernel_code_hash("k_decode_idx", lib="/nonexistent.so") is None

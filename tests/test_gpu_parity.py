@@ -360,7 +360,7 @@ def _run_variant_alone(frame, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["default", "idx1", "idx2", "pp2"])
+@pytest.mark.parametrize("variant", ["default", "idx1", "pp2"])
 @pytest.mark.parametrize("kind", ["dense", "mixed", "literal", "rle", "chain"])
 @pytest.mark.parametrize("bmax", [64 << 10, 256 << 10, 4 << 20])
 def test_idx_decoder_alone(kind, bmax, variant):
@@ -434,7 +434,7 @@ def oracle_blocks(frame, nblocks):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("alone", ["default", "idx1", "idx2", "pp2"])
+@pytest.mark.parametrize("alone", ["default", "idx1", "pp2"])
 @pytest.mark.parametrize("name", ["t100k", "t1111k", "b3444k", "z2841", "t300k", "a2246", "z9m"])
 def test_idx_decoder_on_vectors(name, digests, alone):
     """Reference vectors' blocks through the idx decoder (+ retry): every block
