@@ -546,6 +546,19 @@ def bench_real(M, dev, sh, stream, name, bmax, target_bytes=8 << 30, reps=3):
            "match_sources": match_sources(recs),
            "golden": "per-block XXH32 of the output vs the frame's own digests (encoder input / "
                      "content checksum)"}
+    # HBM traffic of k_decode_idx on this class (profiles/pmc_real.json, tools/pmc_real.sh:
+    # FETCH_SIZE x 2 + WRITE_SIZE per launch of 2,048 blocks over the algorithmic bytes of that
+    # launch), when the kernel's machine code is the one the counters were collected on
+    try:
+        pr = json.load(open(os.path.join(ROOT, "profiles", "pmc_real.json")))
+        e = pr["classes"].get(name)
+        if e and "traffic_over_alg" in e and pr.get("kernel_code_sha16") == kernel_code_hash("k_decode_idx"):
+            row["traffic"] = {"hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
+                              "alg_bytes_per_launch": e["alg_bytes_per_launch"],
+                              "traffic_over_alg": e["traffic_over_alg"],
+                              "source": "profiles/pmc_real.json (2,048-block k_decode_idx launch)"}
+    except (OSError, ValueError, KeyError):
+        pass
     del fr, de, d_out
     return row
 
