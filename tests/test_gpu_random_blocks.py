@@ -95,3 +95,13 @@ def test_random_blocks(frames, k, variant):
         assert out[o:o + len(r)] == r, i
         took += 1
     assert took >= len(raws) // 2
+
+
+@pytest.mark.parametrize("k", range(6))
+def test_random_blocks_facade(frames, k):
+    """The same frames through Update at 4 KiB feeds (the lone-block decoder
+    per block, k_decode_pc below 6 KiB compressed): the oracle's trace."""
+    from test_gpu_facade import trace_oracle, trace_ours_ctx
+    frame, raws = frames[k]
+    ours, exact = trace_ours_ctx(frame, 4096)
+    assert ours == trace_oracle(frame, 4096)
