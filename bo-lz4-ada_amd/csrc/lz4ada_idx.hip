@@ -1551,6 +1551,10 @@ __device__ __forceinline__ bool d1_emulable(int32_t mdst, int32_t L, int32_t& li
 		return false;  // it also reads the current round
 	if (L > 0)
 		return lit + 8 * ((L - 1) >> 3) + 8 <= n;
+	if (n1 + mdst == 0) {  // the round's first output: nothing written past its frontier yet,
+		lit = D1_QBIAS << 3;  // the read is the previous round's bytes -- plain history (pad 0)
+		return true;
+	}
 	if (pml <= 0)
 		return false;  // the previous match is not known here
 	const int32_t f = n1 + pmd, raw = f - pof, pad = (8 - (pml & 7)) & 7;

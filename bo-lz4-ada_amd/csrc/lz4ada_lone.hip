@@ -724,6 +724,9 @@ __global__ __launch_bounds__(LT) void k_lone_words(const uint8_t* __restrict__ b
 			const int32_t ovs = 8 * ((L + 7) / 8) - L;
 			if (n1 + oa + L + R[j].ml > off || (L > 0 && c_last + 8 > n)) {
 				bad = true;  // the cases not emulated: the exact path
+			} else if (L == 0 && n1 + oa == 0) {
+				// the round's first output: nothing written past its frontier
+				// yet, so the read is the previous round's bytes (plain history)
 			} else if (L == 0) {
 				// the previous match's overshoot: output bytes q + d + i
 				const int32_t pml = j > 0 ? R[j - 1].ml : 0, pof = j > 0 ? int32_t(R[j - 1].off & 0xFFFFu) : 0;

@@ -372,6 +372,29 @@ def test_facade_linked_d1_without_literals_on_gpu(lit_len, pof, pml, off):
         assert exact == 0, exact
 
 
+def d1_frame_first(off, ml, tail=b"vwxyz"):
+    """A 64 KiB block, then a block whose FIRST sequence is a match off back
+    with no literals: the round's first output, so nothing lies past the
+    frontier yet and the read is the previous round's bytes."""
+    import struct
+    comp0, raw0 = lz4ada.gen_block(1, 1234, 65536)
+    comp1 = (bytes([min(ml - 4, 15)]) + struct.pack("<H", off) + (bytes([ml - 19]) if ml >= 19 else b"") +
+             bytes([len(tail) << 4]) + tail)
+    frame, _ = lz4frame.build_frame([(comp0, raw0, False), (comp1, b"", False)], 64 * KiB, indep=False)
+    return frame
+
+
+@pytest.mark.parametrize("off,ml", [(65529, 4), (65533, 10), (65535, 40)])
+def test_facade_linked_d1_as_first_output_on_gpu(off, ml):
+    """A D1-range read as the round's first output (no overshoot exists):
+    plain history on the GPU, no exact block, the oracle's trace."""
+    frame = d1_frame_first(off, ml)
+    for feed in (0, 4096):
+        ours, exact = trace_ours_ctx(frame, feed)
+        assert ours == trace_oracle(frame, feed)
+        assert exact == 0, exact
+
+
 def test_facade_linked_d1_without_literals_goes_exact():
     """Quirk D1 after a match whose source overlaps its output (offset 3,
     5 bytes: a repeating part, whose overshoot reads bytes that same call

@@ -163,7 +163,9 @@ def d1_emulable(payload, n1, oph):
                 return False
             continue
         if prev is None:
-            return False
+            if n1 + m != 0:
+                return False
+            continue  # the round's first output: plain history
         pm, po, pml = prev
         f, pad = n1 + pm, (8 - pml % 8) % 8
         raw = f - po
@@ -369,6 +371,19 @@ def test_d1_without_literals_in_bulk(lit_len, pof, pml, off):
     blocks = [(frame[d.in_off:d.in_off + d.in_len], b"\0" * (65536 if k == 0 else len(ref) - 65536))
               for k, d in enumerate(descs[:info.nblocks])]
     assert lz4ada.last_path() == want_path(blocks, 64 * KiB)
+    assert lz4ada.last_path() == lz4ada.PATH_LINKED
+
+
+@pytest.mark.parametrize("off,ml", [(65529, 4), (65533, 10), (65535, 40)])
+def test_d1_as_first_output_in_bulk(off, ml):
+    """A D1-range read as the round's first output (test_gpu_facade.py's
+    d1_frame_first): plain history, the whole frame on the bulk path."""
+    from test_gpu_facade import d1_frame_first
+    frame = d1_frame_first(off, ml)
+    st, ref, msg = oracle(frame)
+    assert st == O.OK, msg
+    out, _ = lz4ada.decode_frame(frame)
+    assert out == ref
     assert lz4ada.last_path() == lz4ada.PATH_LINKED
 
 

@@ -60,7 +60,9 @@ def emulate(blocks, ref, l0=True):
                     ovs = 8 * ((L + 7) // 8) - L
                     if d < ovs: k1 = min(ovs - d, ml); src = ("pay", lit + L + d); reasons["L>0 k1>0"] += 1
                 else:
-                    if prev is None:
+                    if prev is None and n1 + m == 0:
+                        reasons["L0 round's first output"] += 1  # plain history, nothing to emulate
+                    elif prev is None:
                         declined = declined or "L0 first in block"
                     elif not l0:
                         declined = declined or "L0"
