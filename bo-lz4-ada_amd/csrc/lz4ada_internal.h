@@ -95,7 +95,7 @@ enum DecVariant : int { DEC_PC = 0, DEC_IDX = 3, DEC_IDX_ALONE = 4,
                         DEC_PP2_ALONE = 9,
                         // k_index then k_decode_idx's pass 2, two launches (per-pass counters)
                         DEC_IDX_SPLIT = 10 };
-int idx_fused_mode(uint32_t nblocks);  // 3: k_decode_idx, 4: k_decode_idx2, 5: k_decode_pp2 (lz4ada_idx.hip)
+int idx_fused_mode(uint32_t nblocks);  // 3: k_decode_idx, 5: k_decode_pp2 (4, round 4's k_decode_idx2, is retired) (lz4ada_idx.hip)
 const char* idx_fused_kernel_name(uint32_t nblocks);  // the kernel idx_fused_mode picks
 
 hipError_t launch_decode_variant(const uint8_t* d_frame, uint64_t frame_len,

@@ -376,7 +376,7 @@ def test_idx_decoder_alone(kind, bmax, variant):
         blocks.append(lz4ada.gen_block(lz4ada.GEN_KINDS[kind], 900 + j, min(n, bmax)))
     frame, raw = lz4frame.build_frame([(c, r, False) for c, r in blocks], bmax, indep=True)
     v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
-         "idx2": lz4ada.DECODE_IDX2_ALONE, "pp2": lz4ada.DECODE_PP2_ALONE}[variant]
+         "pp2": lz4ada.DECODE_PP2_ALONE}[variant]
     descs, st, out = _run_variant_alone(frame, v)
     bad = []
     for i, (c, r) in enumerate(blocks):
@@ -443,7 +443,7 @@ def test_idx_decoder_on_vectors(name, digests, alone):
     frame = read_vector(name, "lz4")
     info, _ = lz4ada.frame_index(frame)
     v = {"default": lz4ada.DECODE_IDX_ALONE, "idx1": lz4ada.DECODE_IDX1_ALONE,
-         "idx2": lz4ada.DECODE_IDX2_ALONE, "pp2": lz4ada.DECODE_PP2_ALONE}[alone]
+         "pp2": lz4ada.DECODE_PP2_ALONE}[alone]
     descs, st, out = _run_variant_alone(frame, v)
     for i in range(info.nblocks):
         assert st[i].code in (0, lz4ada.DS_RETRY, lz4ada.DS_SPARSE), (i, st[i].code)

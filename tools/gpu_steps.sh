@@ -15,7 +15,7 @@
 #   linked   tools/linked_time.py (configs[4]: mixed, dense, chain; then the mixed phases)
 #   classes  tools/time_decode.py per content class (decoder alone and product step)
 #   pp2      the pipelined two-wave decoder: its parity tests, then timed beside
-#            k_decode_idx2 / k_decode_idx at 1,024 and 2,048 blocks
+#            k_decode_idx at 1,024 and 2,048 blocks
 #   gathers  tools/gathers.py (needs the LZ4ADA_IDX_GATHERS variant build)
 #
 # Every step runs under its own time limit; the first failure ends the run.
@@ -77,7 +77,7 @@ for step in "$@"; do
       -k "pp2" > $O/${TAG}_pp2tests.log 2>&1 || fail pp2-tests $O/${TAG}_pp2tests.log
     tail -2 $O/${TAG}_pp2tests.log
     for k in mixed dense; do for nb in 1024 2048; do
-      timeout -k 10 200 python tools/time_decode.py --kind $k --blocks $nb --variant idx2,pp2,idx1 --check 2>&1 \
+      timeout -k 10 200 python tools/time_decode.py --kind $k --blocks $nb --variant pp2,idx1 --check 2>&1 \
         | grep -v amdgpu || fail pp2-time /dev/null
     done; done ;;
   gathers)

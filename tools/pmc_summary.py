@@ -26,7 +26,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import kernel_code_hash  # noqa: E402
-KERNELS = ("k_decode_idx_zl", "k_decode_idx_lk", "k_decode_idx2", "k_decode_pp2", "k_decode_idx", "k_index", "k_decode_sparse", "k_decode_pc", "k_decode_blocks",
+KERNELS = ("k_decode_idx_zl", "k_decode_idx_lk", "k_decode_pp2", "k_decode_idx", "k_index", "k_decode_sparse", "k_decode_pc", "k_decode_blocks",
            "k_lone_windows", "k_lone_chain", "k_lone_words", "k_lone_resolve",
            "k_link_fill", "k_link_init", "k_link_jump", "k_link_tail",
            "k_xxh32_rows", "k_serial_block", "k_xxh32_update",

@@ -25,7 +25,7 @@ import lz4frame  # noqa: E402
 VARIANTS = {"pc": lz4ada.DECODE_PC,
             "idx": lz4ada.DECODE_IDX, "idx_alone": lz4ada.DECODE_IDX_ALONE,
             "idx_sparse": lz4ada.DECODE_IDX_SPARSE,
-            "idx1": lz4ada.DECODE_IDX1_ALONE, "idx2": lz4ada.DECODE_IDX2_ALONE,
+            "idx1": lz4ada.DECODE_IDX1_ALONE,
             "pp2": lz4ada.DECODE_PP2_ALONE, "split": lz4ada.DECODE_IDX_SPLIT}
 
 
